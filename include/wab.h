@@ -1,0 +1,171 @@
+/*
+ * wab.h — C-ABI of the MI355X-native batched Wolves-and-Bushes step.
+ *
+ * This is the drop-in boundary for the hot path of johnmatthewtennant/wab-gym:
+ * `WolvesAndBushesEnv.reset()/step()` (wab_env.py:103-342) with a leading batch
+ * dimension.  Plain pointers and sizes only; every device pointer is a HIP device
+ * address (e.g. a torch tensor's data_ptr()), every `stream` a hipStream_t (NULL =
+ * the legacy default stream).  The caller owns all I/O buffers; the handle owns
+ * per-env state in HBM and the constant tables.  Calls are stream-ordered and
+ * asynchronous unless stated otherwise.  A handle is not thread-safe.  All calls
+ * return 0 on success and a negative WAB_E_* code on failure; the message is
+ * available from wab_last_error() (thread-local).
+ *
+ * Reference interface replaced (file:line in /root/reference):
+ *   wab_config            <- default_game_options                   wab_env.py:11-39
+ *   wab_create            <- WolvesAndBushesEnv.__init__            wab_env.py:106-186
+ *                            (odd width/height check                wab_env.py:147-148)
+ *   wab_reset             <- WolvesAndBushesEnv.reset               wab_env.py:231-248
+ *   wab_step              <- WolvesAndBushesEnv.step                wab_env.py:250-342
+ *   wab_obs               <- _get_obs 7-tuple                        wab_env.py:359-385
+ *   wab_rollout           <- the per-step loop of actor_critic.main  actor_critic.py:185-200
+ *                            with pre-chosen actions (T fused steps)
+ *   wab_destroy           <- (gym.Env.close; nothing to free in the reference)
+ */
+#ifndef WAB_H_
+#define WAB_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WAB_ABI_VERSION 1
+#define WAB_MAX_WOLF_SLOTS 32 /* largest per-env live-wolf slot count (wab_config.wolf_slots) */
+#define WAB_MAX_VIEW 63       /* largest odd width/height accepted */
+
+/* error codes */
+#define WAB_OK 0
+#define WAB_E_INVALID (-1)    /* bad argument (ValueError in the reference) */
+#define WAB_E_HIP (-2)        /* HIP runtime error */
+#define WAB_E_NOMEM (-3)
+#define WAB_E_STATE (-4)      /* call not allowed in the handle's current state */
+
+/* Game options, field-for-field `default_game_options` (wab_env.py:11-39).
+ * Booleans are int32 0/1.  `None` options of the reference are spelled with the
+ * *_random flags.  The last block are batched-surface extensions. */
+typedef struct wab_config {
+  double reward_per_turn;          /* 0 */
+  double reward_for_being_killed;  /* -1 */
+  double reward_for_starving;      /* -1 */
+  double reward_for_finishing;     /* 1 */
+  double reward_for_eating;        /* 0.1 */
+  int32_t gatherer_only;           /* 0  (action table wab_env.py:149-159) */
+  int32_t lookout_only;            /* 1  (action table wab_env.py:160-170; eat gate :302) */
+  int32_t restrict_view;           /* 0  (masks wab_env.py:109-139, applied :344-357) */
+  int32_t starting_role;           /* 1 */
+  int32_t starting_role_random;    /* 1 <=> starting_role None (wab_env.py:598-599) */
+  int32_t starting_food_random;    /* 1 <=> starting_food None (wab_env.py:596-597) */
+  double starting_food;            /* 1.0 */
+  int32_t max_turns;               /* 80 */
+  int32_t height;                  /* 11, odd */
+  int32_t width;                   /* 11, odd */
+  int32_t max_berries_per_bush;    /* 200, <= 255 */
+  double bush_power;               /* 100 (informational: the threshold table carries it) */
+  int32_t turns_to_fill_food;      /* 8 */
+  int32_t turns_to_empty_food;     /* 40 */
+  int32_t wolf_spawn_margin;       /* 1 */
+  double chance_wolf_on_square;    /* 0.001 (spawn test is u < chance/2, wab_env.py:573) */
+  double wolf_chance_to_despawn;   /* 0.05 (keep test is u > chance, wab_env.py:263) */
+  int32_t wolves;                  /* 1 */
+  int32_t wolves_can_move;         /* 1 */
+  int32_t god_mode;                /* 0 (hidden key, wab_env.py:292) */
+  /* ---- batched-surface extensions ---- */
+  int32_t autoreset;               /* 1: a done env is reset inside the same step call */
+  int32_t plane_stride;            /* bytes per grid row in `planes` (>= height; 0 = height) */
+  int32_t eaten_capacity;          /* eaten-tile log slots per env (0 = max(max_turns, 1)) */
+  int32_t wolf_slots;              /* live-wolf slots per env: 8 (0 = 8), 16 or 32; a spawn
+                                    * beyond them is dropped and counted (wolf_overflow) */
+  /* T_k (k = 1..max_berries_per_bush): the smallest 53-bit U with
+   * round((U * 2^-53) ** bush_power * max_berries_per_bush) >= k, computed by the
+   * host with the reference's own numpy arithmetic (wab_env.py:632-635).
+   * Copied at wab_create. */
+  const uint64_t* bush_thresholds;
+} wab_config;
+
+/* One observation batch — the reference's 7-tuple (wab_env.py:374-385) with a
+ * leading batch dimension.  All device pointers, caller-owned.
+ *   planes     [B][3][width][plane_stride] u8 0/1: wolf, bush, ostrich grids.
+ *              Axis 1 is x, cell [width/2 + (ox - x)][height/2 + (oy - y)]
+ *              (wab_env.py:403-409); padding bytes are written as 0.
+ *   food_turns [B] u8  ceil(food * turns_to_empty_food)   (wab_env.py:450-452)
+ *   role       [B] u8                                      (wab_env.py:390-391)
+ *   status     [B] u8  0 alive, 1 starved, 2 killed        (wab_env.py:387-388)
+ * view_mask (7th element) is a pure function of role and options; the host side
+ * derives it (wab_env.py:360-368). */
+typedef struct wab_obs {
+  uint8_t* planes;
+  uint8_t* food_turns;
+  uint8_t* role;
+  uint8_t* status;
+} wab_obs;
+
+/* Device-side counters, read back by wab_get_counters (synchronising). */
+typedef struct wab_counters {
+  uint64_t wolf_overflow;    /* wolves dropped because all wolf_slots slots were live */
+  uint64_t eaten_overflow;   /* eats not logged because the eaten-tile log was full */
+  uint64_t bad_actions;      /* actions outside [0, n_actions): treated as no-op */
+  uint64_t steps;            /* env-steps executed */
+  uint64_t resets;           /* env resets executed */
+} wab_counters;
+
+typedef struct wab_handle wab_handle;
+
+/* ABI version compiled into the library (== WAB_ABI_VERSION). */
+int wab_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* wab_last_error(void);
+
+/* Number of actions of the table selected by the options (5 or 6, wab_env.py:149-182). */
+int wab_num_actions(const wab_config* cfg);
+
+/* Validate options and allocate state for `batch` envs on HIP device `device`.
+ * Env i has global id env_id_base + i; every random draw is keyed by
+ * (seed, global id, episode, ...), so results do not depend on batch size, shard
+ * count or device.  Synchronous.  No env is reset yet: call wab_reset first. */
+int wab_create(const wab_config* cfg, int64_t batch, uint64_t seed, int64_t env_id_base,
+               int device, wab_handle** out);
+
+/* Free the handle and its device state (synchronises the device). */
+int wab_destroy(wab_handle* h);
+
+/* Reset envs (all, or those with mask[i] != 0; mask is a device pointer or NULL) and
+ * write their observations into `obs` (other envs' obs entries are left untouched).
+ * The first reset of an env is episode 0; each later reset increments its episode. */
+int wab_reset(wab_handle* h, const uint8_t* mask, const wab_obs* obs, void* stream);
+
+/* One step of every env.  actions: [B] int8 device.  Writes obs, reward [B] f32
+ * (the reference's double reward rounded to f32), done [B] u8.
+ * With cfg.autoreset, an env that is done is reset in the same call: `obs` then holds
+ * the new episode's first observation and, if `terminal` is non-NULL, the step's own
+ * observation is written to `terminal` (only the done envs' entries are written).
+ * Without autoreset the env keeps stepping after done exactly as the reference does
+ * (stepping after done is not guarded, wab_env.py:250). */
+int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward,
+             uint8_t* done, const wab_obs* terminal, void* stream);
+
+/* T fused steps in one launch (state stays in registers between steps).
+ * actions [T][B] int8; obs planes [T][B][3][width][plane_stride] and the scalar
+ * arrays [T][B] (an obs "sequence"); reward/done [T][B].  Equivalent to T calls of
+ * wab_step with terminal = NULL. */
+int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq,
+                float* reward, uint8_t* done, void* stream);
+
+/* Read the device counters (synchronises `stream`). */
+int wab_get_counters(wab_handle* h, wab_counters* out, void* stream);
+
+/* Copy hidden per-env state to HOST arrays (any may be NULL; synchronises `stream`):
+ * food [B] f64, x/y [B] i32, turn [B] i32, n_wolves [B] i32, episode [B] u32. */
+int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* turn,
+                  int32_t* n_wolves, uint32_t* episode, void* stream);
+
+/* Batch size and global-id base of a handle. */
+int64_t wab_batch(const wab_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAB_H_ */

@@ -1,0 +1,121 @@
+"""ctypes binding of the C oracle (oracle/wab_oracle.c).
+
+TEST INFRASTRUCTURE: imported only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The oracle is the checker; the product (wab_gym_amd) never loads it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libwab_oracle.so")
+
+_lib = None
+
+
+def build(quiet=True):
+    subprocess.run(["make", "-C", HERE], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+def _stale():
+    srcs = [os.path.join(HERE, f) for f in ("wab_oracle.c", "wab_oracle.h", "Makefile")]
+    srcs.append(os.path.join(os.path.dirname(HERE), "include", "wab.h"))
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.exists(s) and os.path.getmtime(s) > t for s in srcs)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or _stale():
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.wabo_create.restype = P
+        L.wabo_create.argtypes = [P, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64]
+        L.wabo_destroy.argtypes = [P]
+        L.wabo_num_actions.argtypes = [P]
+        L.wabo_reset.argtypes = [P] * 6
+        L.wabo_step.argtypes = [P] * 12 + [ctypes.c_int]
+        L.wabo_get_state.argtypes = [P] * 7
+        L.wabo_episode_key.restype = ctypes.c_uint64
+        L.wabo_episode_key.argtypes = [ctypes.c_uint64] * 3
+        L.wabo_draw_U.restype = ctypes.c_uint64
+        L.wabo_draw_U.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.c_int64, ctypes.c_uint32]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class OracleBatch:
+    """B envs on the host CPU, same array layouts as wab.h's wab_obs."""
+
+    def __init__(self, options=None, batch=1, seed=0x5EED, env_id_base=0, autoreset=True,
+                 plane_stride=0):
+        from wab_gym_amd.options import make_config  # config translation only (no product code path)
+
+        self.cfg, self._keep = make_config(options, autoreset=autoreset, plane_stride=plane_stride)
+        self.options = self._keep[1]
+        self.B = int(batch)
+        self.W, self.H = self.cfg.width, self.cfg.height
+        self.S = plane_stride or self.H
+        self.h = lib().wabo_create(ctypes.addressof(self.cfg), self.B, seed, env_id_base)
+        if not self.h:
+            raise ValueError("oracle rejected the options")
+        self.n_actions = lib().wabo_num_actions(self.h)
+        shape = (self.B, 3, self.W, self.S)
+        self.planes = np.zeros(shape, np.uint8)
+        self.food_turns = np.zeros(self.B, np.uint8)
+        self.role = np.zeros(self.B, np.uint8)
+        self.status = np.zeros(self.B, np.uint8)
+        self.reward = np.zeros(self.B, np.float32)
+        self.done = np.zeros(self.B, np.uint8)
+        self.t_planes = np.zeros(shape, np.uint8)
+        self.t_food_turns = np.zeros(self.B, np.uint8)
+        self.t_role = np.zeros(self.B, np.uint8)
+        self.t_status = np.zeros(self.B, np.uint8)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().wabo_destroy(self.h)
+            self.h = None
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        lib().wabo_reset(self.h, _p(m), _p(self.planes), _p(self.food_turns), _p(self.role),
+                         _p(self.status))
+        return self.planes, self.food_turns, self.role, self.status
+
+    def step(self, actions, nthreads=1):
+        a = np.ascontiguousarray(actions, dtype=np.int8)
+        lib().wabo_step(self.h, _p(a), _p(self.planes), _p(self.food_turns), _p(self.role),
+                        _p(self.status), _p(self.reward), _p(self.done), _p(self.t_planes),
+                        _p(self.t_food_turns), _p(self.t_role), _p(self.t_status), int(nthreads))
+        return self.planes, self.food_turns, self.role, self.status, self.reward, self.done
+
+    def state(self):
+        food = np.zeros(self.B, np.float64)
+        x = np.zeros(self.B, np.int32)
+        y = np.zeros(self.B, np.int32)
+        turn = np.zeros(self.B, np.int32)
+        nw = np.zeros(self.B, np.int32)
+        ep = np.zeros(self.B, np.uint32)
+        lib().wabo_get_state(self.h, _p(food), _p(x), _p(y), _p(turn), _p(nw), _p(ep))
+        return dict(food=food, x=x, y=y, turn=turn, n_wolves=nw, episode=ep)
+
+
+def episode_key(seed, env, episode):
+    return int(lib().wabo_episode_key(seed, env, episode))
+
+
+def draw_U(ek, site, turn, x, y, k=0):
+    return int(lib().wabo_draw_U(ek, site, turn, x, y, k))

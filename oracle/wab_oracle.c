@@ -1,0 +1,369 @@
+/*
+ * wab_oracle.c — TEST INFRASTRUCTURE: scalar C restatement of the reference step.
+ *
+ * Restates wab_env.py (johnmatthewtennant/wab-gym) `reset` (:231-248) and `step`
+ * (:250-342) for one env at a time, looping over a batch.  Random draws follow the keyed
+ * RNG defined in oracle/keyed_rng.py (the same definition the golden vectors were
+ * generated under).  Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).
+ *
+ * Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+ */
+#include "wab_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ keyed RNG */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+uint64_t wabo_episode_key(uint64_t seed, uint64_t env, uint64_t episode) {
+  uint64_t a = mix64(seed + 0x9E3779B97F4A7C15ULL);
+  uint64_t b = mix64(a ^ env);
+  return mix64(b ^ episode);
+}
+
+uint64_t wabo_draw_U(uint64_t ek, uint32_t site, int64_t turn, int64_t x, int64_t y, uint32_t k) {
+  uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+  uint32_t xy = (uint32_t)(x & 0xFFFF) | ((uint32_t)(y & 0xFFFF) << 16);
+  uint32_t ts = (site & 0xFu) | ((k & 0xFFu) << 4) | ((uint32_t)(turn & 0xFFFFF) << 12);
+  uint32_t h1 = fmix32(xy ^ b0);
+  uint32_t hi = fmix32(h1 ^ ts ^ b1);
+  uint32_t rot = (ts << 16) | (ts >> 16);
+  uint32_t lo = fmix32(h1 ^ rot ^ b0 ^ 0x9E3779B9u);
+  return ((uint64_t)hi << 21) | (uint64_t)(lo >> 11);
+}
+
+enum { SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5 };
+
+/* ------------------------------------------------------------------ state */
+typedef struct { int32_t x, y; } xy_t;
+typedef struct { int32_t x, y, rem; } eaten_t;
+
+typedef struct {
+  int64_t env_id;
+  int64_t episode; /* -1 before the first reset */
+  uint64_t ek;
+  int32_t turn, x, y, role, status;
+  double food;
+  int nw, capw;
+  xy_t* wolves;
+  int ne, cape;
+  eaten_t* eaten;
+} oenv;
+
+struct wabo_batch {
+  wab_config cfg;
+  uint64_t* thresholds;
+  int64_t batch;
+  uint64_t seed;
+  int n_actions;
+  int act_dx[6], act_dy[6], act_role[6]; /* act_role -1 = NaN (no role change) */
+  uint64_t keep_gt, spawn_lt;
+  double fill, hunger;
+  int stride, plane_bytes, obs_bytes;
+  oenv* envs;
+};
+
+/* masks wab_env.py:109-139 */
+static const uint8_t LOOKOUT_MASK[11][11] = {
+    {1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 1}, {1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 1},
+    {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1}, {1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 1},
+    {1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 1}};
+static const uint8_t GATHERER_MASK[11][11] = {
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1}, {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1},
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1}, {1, 1, 1, 1, 0, 0, 0, 1, 1, 1, 1},
+    {1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 1}, {1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 1},
+    {1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 1}, {1, 1, 1, 1, 0, 0, 0, 1, 1, 1, 1},
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1}, {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1},
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1}};
+
+/* number of k with U >= T_k: the reference's round(u**power * max) (wab_env.py:631-635) */
+static int bush_value(const wabo_batch* b, uint64_t U) {
+  int lo = 0, hi = b->cfg.max_berries_per_bush; /* count of thresholds <= U */
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (b->thresholds[mid] <= U) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+/* remaining berries at a tile: eaten log, else the tile's generated value (wab_env.py:613-629) */
+static int bush_remaining(const wabo_batch* b, const oenv* e, int32_t x, int32_t y) {
+  for (int i = 0; i < e->ne; ++i)
+    if (e->eaten[i].x == x && e->eaten[i].y == y) return e->eaten[i].rem;
+  return bush_value(b, wabo_draw_U(e->ek, SITE_BUSH, 0, x, y, 0));
+}
+
+static void set_remaining(oenv* e, int32_t x, int32_t y, int rem) {
+  for (int i = 0; i < e->ne; ++i)
+    if (e->eaten[i].x == x && e->eaten[i].y == y) { e->eaten[i].rem = rem; return; }
+  if (e->ne == e->cape) {
+    e->cape = e->cape ? 2 * e->cape : 16;
+    e->eaten = (eaten_t*)realloc(e->eaten, sizeof(eaten_t) * (size_t)e->cape);
+  }
+  e->eaten[e->ne].x = x; e->eaten[e->ne].y = y; e->eaten[e->ne].rem = rem;
+  e->ne++;
+}
+
+static void push_wolf(oenv* e, int32_t x, int32_t y) {
+  if (e->nw == e->capw) {
+    e->capw = e->capw ? 2 * e->capw : 8;
+    e->wolves = (xy_t*)realloc(e->wolves, sizeof(xy_t) * (size_t)e->capw);
+  }
+  e->wolves[e->nw].x = x; e->wolves[e->nw].y = y;
+  e->nw++;
+}
+
+/* ------------------------------------------------------------------ construction */
+wabo_batch* wabo_create(const wab_config* cfg, int64_t batch, uint64_t seed, int64_t env_id_base) {
+  if (cfg->width % 2 == 0 || cfg->height % 2 == 0) return NULL; /* wab_env.py:147-148 */
+  wabo_batch* b = (wabo_batch*)calloc(1, sizeof(wabo_batch));
+  b->cfg = *cfg;
+  b->batch = batch;
+  b->seed = seed;
+  int nb = cfg->max_berries_per_bush;
+  b->thresholds = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(nb > 0 ? nb : 1));
+  for (int k = 0; k < nb; ++k) b->thresholds[k] = cfg->bush_thresholds[k];
+  b->cfg.bush_thresholds = NULL;
+  /* action tables wab_env.py:149-182: up (y+1), right (x+1), down (y-1), left (x-1) */
+  static const int dx[6] = {0, 1, 0, -1, 0, 0}, dy[6] = {1, 0, -1, 0, 0, 0};
+  for (int a = 0; a < 6; ++a) { b->act_dx[a] = dx[a]; b->act_dy[a] = dy[a]; b->act_role[a] = -1; }
+  if (cfg->gatherer_only) { b->n_actions = 5; b->act_role[4] = 1; }
+  else if (cfg->lookout_only) { b->n_actions = 5; b->act_role[4] = 0; }
+  else { b->n_actions = 6; b->act_role[4] = 1; b->act_role[5] = 0; }
+  /* u > despawn keeps a wolf (:263); u < chance/2 spawns one (:573) */
+  b->keep_gt = (uint64_t)floor(ldexp(cfg->wolf_chance_to_despawn, 53));
+  b->spawn_lt = (uint64_t)ceil(ldexp(cfg->chance_wolf_on_square / 2.0, 53));
+  b->fill = 1.0 / (double)cfg->turns_to_fill_food;    /* :307-309 */
+  b->hunger = 1.0 / (double)cfg->turns_to_empty_food; /* :316 */
+  b->stride = cfg->plane_stride > 0 ? cfg->plane_stride : cfg->height;
+  b->plane_bytes = cfg->width * b->stride;
+  b->obs_bytes = 3 * b->plane_bytes;
+  b->envs = (oenv*)calloc((size_t)batch, sizeof(oenv));
+  for (int64_t i = 0; i < batch; ++i) {
+    b->envs[i].env_id = env_id_base + i;
+    b->envs[i].episode = -1;
+  }
+  return b;
+}
+
+void wabo_destroy(wabo_batch* b) {
+  if (!b) return;
+  for (int64_t i = 0; i < b->batch; ++i) { free(b->envs[i].wolves); free(b->envs[i].eaten); }
+  free(b->envs);
+  free(b->thresholds);
+  free(b);
+}
+
+int wabo_num_actions(const wabo_batch* b) { return b->n_actions; }
+
+/* ------------------------------------------------------------------ observation */
+/* grids from the snapshot (wab_env.py:393-444): planes are [3][W][stride] */
+static void render_planes(const wabo_batch* b, const oenv* e, int center_rem, uint8_t* out) {
+  const int W = b->cfg.width, H = b->cfg.height, S = b->stride;
+  const int cw = W / 2, ch = H / 2;
+  memset(out, 0, (size_t)b->obs_bytes);
+  uint8_t* wolf = out;
+  uint8_t* bush = out + b->plane_bytes;
+  uint8_t* ost = out + 2 * b->plane_bytes;
+  for (int i = 0; i < e->nw; ++i) {
+    int ddx = e->x - e->wolves[i].x, ddy = e->y - e->wolves[i].y;
+    if (abs(ddx) <= cw && abs(ddy) <= ch) wolf[(ddx + cw) * S + (ddy + ch)] = 1;
+  }
+  for (int i = 0; i < W; ++i)
+    for (int j = 0; j < H; ++j) {
+      int32_t bx = e->x - (i - cw), by = e->y - (j - ch);
+      int rem = (i == cw && j == ch) ? center_rem : bush_remaining(b, e, bx, by);
+      bush[i * S + j] = rem > 0;
+    }
+  ost[cw * S + ch] = 1; /* the ostrich itself, delta 0 */
+}
+
+/* mask_grid (wab_env.py:344-357) with the fresh role; only when restrict_view */
+static void mask_planes(const wabo_batch* b, int role, uint8_t* out) {
+  if (!b->cfg.restrict_view) return;
+  const uint8_t(*m)[11] = role == 1 ? GATHERER_MASK : LOOKOUT_MASK;
+  for (int p = 0; p < 3; ++p)
+    for (int i = 0; i < 11; ++i)
+      for (int j = 0; j < 11; ++j)
+        if (m[i][j]) out[p * b->plane_bytes + i * b->stride + j] = 0;
+}
+
+static void scalars(const wabo_batch* b, const oenv* e, uint8_t* food_turns, uint8_t* role,
+                    uint8_t* status) {
+  food_turns[0] = (uint8_t)(int)ceil(e->food * (double)b->cfg.turns_to_empty_food); /* :452 */
+  role[0] = (uint8_t)e->role;
+  status[0] = (uint8_t)e->status;
+}
+
+/* ------------------------------------------------------------------ reset (wab_env.py:231-248) */
+static void reset_one(wabo_batch* b, oenv* e, uint8_t* planes, uint8_t* food_turns, uint8_t* role,
+                      uint8_t* status) {
+  const wab_config* c = &b->cfg;
+  e->episode += 1;
+  e->ek = wabo_episode_key(b->seed, (uint64_t)e->env_id, (uint64_t)e->episode);
+  e->turn = 0;
+  e->x = 0; e->y = 0;
+  e->status = 0;
+  /* spawn_ostriches :595-611 */
+  e->food = c->starting_food_random
+                ? (double)wabo_draw_U(e->ek, SITE_START_FOOD, 0, 0, 0, 0) * 0x1p-53
+                : c->starting_food;
+  e->role = c->starting_role_random
+                ? (int)floor((double)wabo_draw_U(e->ek, SITE_START_ROLE, 0, 0, 0, 0) * 0x1p-53 * 2.0)
+                : c->starting_role;
+  e->nw = 0;
+  e->ne = 0;
+  /* generate_bushes :613-629 is implicit (tile function) */
+  if (c->wolves) { /* initialize_wolves :578-593: every visible tile, turn 0 */
+    const int cw = c->width / 2, ch = c->height / 2;
+    for (int tx = -cw; tx <= cw; ++tx)
+      for (int ty = -ch; ty <= ch; ++ty)
+        if (wabo_draw_U(e->ek, SITE_SPAWN, 0, tx, ty, 0) < b->spawn_lt) push_wolf(e, tx, ty);
+  }
+  int center = bush_remaining(b, e, 0, 0);
+  render_planes(b, e, center, planes);
+  mask_planes(b, e->role, planes);
+  scalars(b, e, food_turns, role, status);
+}
+
+void wabo_reset(wabo_batch* b, const uint8_t* mask, uint8_t* planes, uint8_t* food_turns,
+                uint8_t* role, uint8_t* status) {
+  for (int64_t i = 0; i < b->batch; ++i) {
+    if (mask && !mask[i]) continue;
+    reset_one(b, &b->envs[i], planes + i * b->obs_bytes, food_turns + i, role + i, status + i);
+  }
+}
+
+/* ------------------------------------------------------------------ step (wab_env.py:250-342) */
+static void step_one(wabo_batch* b, oenv* e, int a, uint8_t* planes, uint8_t* food_turns,
+                     uint8_t* role, uint8_t* status, float* reward_out, uint8_t* done_out) {
+  const wab_config* c = &b->cfg;
+  double reward = 0.0;                                    /* :251 */
+  e->turn += 1;                                           /* :252 */
+  if (a >= 0 && a < b->n_actions) {                       /* :253-258 */
+    e->x += b->act_dx[a];
+    e->y += b->act_dy[a];
+    if (b->act_role[a] >= 0) e->role = b->act_role[a];
+  }
+  /* :259 generate_bushes — implicit */
+  /* :262-264 despawn: one draw per wolf in list order, keyed by its tile and its
+   * occurrence index k among co-located wolves; decide all, then compact (stable) */
+  {
+    int n = 0;
+    uint8_t keep[1024];
+    uint8_t* kp = e->nw <= 1024 ? keep : (uint8_t*)malloc((size_t)e->nw);
+    for (int i = 0; i < e->nw; ++i) {
+      uint32_t k = 0;
+      for (int j = 0; j < i; ++j)
+        if (e->wolves[j].x == e->wolves[i].x && e->wolves[j].y == e->wolves[i].y) ++k;
+      kp[i] = wabo_draw_U(e->ek, SITE_DESPAWN, e->turn, e->wolves[i].x, e->wolves[i].y, k) >
+              b->keep_gt;
+    }
+    for (int i = 0; i < e->nw; ++i)
+      if (kp[i]) e->wolves[n++] = e->wolves[i];
+    if (kp != keep) free(kp);
+    e->nw = n;
+  }
+  /* :267-286 pursuit: each wolf one axis step toward the ostrich, ties along x */
+  if (c->wolves_can_move) {
+    for (int i = 0; i < e->nw; ++i) {
+      int ddx = e->x - e->wolves[i].x, ddy = e->y - e->wolves[i].y;
+      if (abs(ddx) >= abs(ddy)) e->wolves[i].x += (ddx > 0) - (ddx < 0);
+      else e->wolves[i].y += (ddy > 0) - (ddy < 0);
+    }
+  }
+  /* :289 snapshot S: wolves now, bushes with food > 0 now, status/role now */
+  const int status_snap = e->status;
+  const int role_snap = e->role;
+  const int center_rem = bush_remaining(b, e, e->x, e->y);
+  render_planes(b, e, center_rem, planes);
+  /* :291-297 kill */
+  if (!c->god_mode) {
+    for (int i = 0; i < e->nw; ++i)
+      if (e->wolves[i].x == e->x && e->wolves[i].y == e->y) { e->status = 2; break; }
+  }
+  /* :299-313 eat (stale snapshot status; clip only in this branch) */
+  if (center_rem > 0 && (role_snap == 1 || c->lookout_only) && status_snap == 0) {
+    e->food += b->fill;
+    e->food = e->food < 0.0 ? 0.0 : (e->food > 1.0 ? 1.0 : e->food);
+    set_remaining(e, e->x, e->y, center_rem - 1);
+    reward += c->reward_for_eating;
+  }
+  e->food -= b->hunger;                                   /* :316 */
+  if (e->food <= 0.0) { e->status = 1; e->food = 0.0; }   /* :319-322 */
+  /* :325-326 spawn_wolves (:527-576): ring around the new position */
+  if (c->wolves) {
+    const int cw = c->width / 2, ch = c->height / 2, m = c->wolf_spawn_margin;
+    for (int tx = e->x - cw - m; tx <= e->x + cw + m; ++tx)
+      for (int ty = e->y - ch - m; ty <= e->y + ch + m; ++ty) {
+        if (tx >= e->x - cw && tx <= e->x + cw && ty >= e->y - ch && ty <= e->y + ch) continue;
+        if (wabo_draw_U(e->ek, SITE_SPAWN, e->turn, tx, ty, 0) < b->spawn_lt) push_wolf(e, tx, ty);
+      }
+  }
+  /* :328-340 reward / done */
+  int done;
+  if (e->status == 0) {
+    if (e->turn >= c->max_turns) { reward += c->reward_for_finishing; done = 1; }
+    else { reward += c->reward_per_turn; done = 0; }
+  } else if (e->status == 1) { reward += c->reward_for_starving; done = 1; }
+  else { reward += c->reward_for_being_killed; done = 1; }
+  /* :342 obs: grids from S (rendered above), scalars fresh */
+  mask_planes(b, e->role, planes);
+  scalars(b, e, food_turns, role, status);
+  *reward_out = (float)reward;
+  *done_out = (uint8_t)done;
+}
+
+void wabo_step(wabo_batch* b, const int8_t* actions, uint8_t* planes, uint8_t* food_turns,
+               uint8_t* role, uint8_t* status, float* reward, uint8_t* done,
+               uint8_t* terminal_planes, uint8_t* terminal_food_turns, uint8_t* terminal_role,
+               uint8_t* terminal_status, int nthreads) {
+  const int64_t B = b->batch;
+  const int ob = b->obs_bytes;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1) if (nthreads > 1)
+  for (int64_t i = 0; i < B; ++i) {
+    oenv* e = &b->envs[i];
+    step_one(b, e, actions[i], planes + i * ob, food_turns + i, role + i, status + i, reward + i,
+             done + i);
+    if (b->cfg.autoreset && done[i]) {
+      if (terminal_planes) {
+        memcpy(terminal_planes + i * ob, planes + i * ob, (size_t)ob);
+        terminal_food_turns[i] = food_turns[i];
+        terminal_role[i] = role[i];
+        terminal_status[i] = status[i];
+      }
+      reset_one(b, e, planes + i * ob, food_turns + i, role + i, status + i);
+    }
+  }
+}
+
+void wabo_get_state(const wabo_batch* b, double* food, int32_t* x, int32_t* y, int32_t* turn,
+                    int32_t* n_wolves, uint32_t* episode) {
+  for (int64_t i = 0; i < b->batch; ++i) {
+    const oenv* e = &b->envs[i];
+    if (food) food[i] = e->food;
+    if (x) x[i] = e->x;
+    if (y) y[i] = e->y;
+    if (turn) turn[i] = e->turn;
+    if (n_wolves) n_wolves[i] = e->nw;
+    if (episode) episode[i] = (uint32_t)e->episode;
+  }
+}

@@ -1,0 +1,59 @@
+"""Replay backends for tests/golden_replay.py: the C oracle (CPU) and the HIP product (GPU)."""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 0x5EED
+
+
+class OracleBackend:
+    def __init__(self, opts, base, n, autoreset, stride, seed=SEED):
+        from oracle.oracle import OracleBatch
+
+        self.o = OracleBatch(opts, n, seed, base, autoreset, stride)
+
+    def reset(self):
+        return tuple(x.copy() for x in self.o.reset())
+
+    def step(self, a):
+        p, f, r, s, rw, d = self.o.step(a)
+        term = (self.o.t_planes.copy(), self.o.t_food_turns.copy(), self.o.t_role.copy(),
+                self.o.t_status.copy())
+        return p.copy(), f.copy(), r.copy(), s.copy(), rw.copy(), d.copy(), term
+
+    def state(self):
+        return self.o.state()
+
+
+class GpuBackend:
+    """The product path: BatchedWolvesAndBushesEnv -> ctypes -> libwab_hip.so (C-ABI)."""
+
+    wolf_slots = 32
+
+    def __init__(self, opts, base, n, autoreset, stride, seed=SEED):
+        from wab_gym_amd.env import BatchedWolvesAndBushesEnv
+
+        self.env = BatchedWolvesAndBushesEnv(opts, num_envs=n, seed=seed, device="cuda:0",
+                                             env_id_base=base, autoreset=autoreset,
+                                             return_terminal=True, plane_stride=stride,
+                                             wolf_slots=self.wolf_slots)
+
+    def _np(self, obs):
+        return (self.env._obs["planes"].cpu().numpy(), obs[3].cpu().numpy(),
+                obs[4].cpu().numpy(), obs[5].cpu().numpy())
+
+    def reset(self):
+        return self._np(self.env.reset())
+
+    def step(self, a):
+        import torch
+
+        obs, rew, done, info = self.env.step(torch.as_tensor(np.asarray(a, np.int64)))
+        planes, f, r, s = self._np(obs)
+        t = self.env._term
+        term = (t["planes"].cpu().numpy(), t["scalars"][0].cpu().numpy(),
+                t["scalars"][1].cpu().numpy(), t["scalars"][2].cpu().numpy())
+        return planes, f, r, s, rew.cpu().numpy(), done.cpu().numpy().astype(np.uint8), term
+
+    def state(self):
+        return self.env.state()

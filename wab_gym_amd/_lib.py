@@ -1,0 +1,81 @@
+"""ctypes binding of the C-ABI in include/wab.h (libwab_hip.so, built in-tree).
+
+There is no fallback: if the HIP library is missing or fails to load, every product
+entry point raises.  torch is imported first so that its bundled HIP runtime
+(SONAME libamdhip64.so.7) is the one the library binds to — one runtime per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libwab_hip.so")
+
+EXPORTED = [
+    "wab_abi_version", "wab_last_error", "wab_num_actions", "wab_create", "wab_destroy",
+    "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
+]
+
+ABI_VERSION = 1
+
+
+class WabObs(ctypes.Structure):
+    _fields_ = [("planes", ctypes.c_void_p), ("food_turns", ctypes.c_void_p),
+                ("role", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
+class WabCounters(ctypes.Structure):
+    _fields_ = [("wolf_overflow", ctypes.c_uint64), ("eaten_overflow", ctypes.c_uint64),
+                ("bad_actions", ctypes.c_uint64), ("steps", ctypes.c_uint64),
+                ("resets", ctypes.c_uint64)]
+
+
+class WabError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libwab_hip.so (raises if it is absent: build it with __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise WabError("libwab_hip.so not built (%s); run `python -c 'import __graft_entry__ as g; "
+                       "g.build()'`" % LIB_PATH)
+    try:
+        import torch  # noqa: F401  (bind to torch's HIP runtime if torch is used)
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    P, I64, U64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32
+    L.wab_abi_version.restype = ctypes.c_int
+    L.wab_last_error.restype = ctypes.c_char_p
+    L.wab_num_actions.argtypes = [P]
+    L.wab_create.argtypes = [P, I64, U64, I64, ctypes.c_int, ctypes.POINTER(P)]
+    L.wab_destroy.argtypes = [P]
+    L.wab_reset.argtypes = [P, P, P, P]
+    L.wab_step.argtypes = [P, P, P, P, P, P, P]
+    L.wab_rollout.argtypes = [P, P, I32, P, P, P, P]
+    L.wab_get_counters.argtypes = [P, P, P]
+    L.wab_get_state.argtypes = [P, P, P, P, P, P, P, P]
+    L.wab_batch.argtypes = [P]
+    L.wab_batch.restype = I64
+    for name in EXPORTED:
+        if name not in ("wab_abi_version", "wab_last_error", "wab_batch"):
+            getattr(L, name).restype = ctypes.c_int
+    if L.wab_abi_version() != ABI_VERSION:
+        raise WabError("libwab_hip.so ABI %d != %d" % (L.wab_abi_version(), ABI_VERSION))
+    _lib = L
+    return L
+
+
+def check(rc, what="wab call"):
+    if rc != 0:
+        msg = load().wab_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError("%s: %s" % (what, msg))
+        raise WabError("%s failed (%d): %s" % (what, rc, msg))

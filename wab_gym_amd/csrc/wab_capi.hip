@@ -1,0 +1,383 @@
+// wab_capi.hip — the C-ABI of include/wab.h on top of the fused HIP kernels.
+//
+// Owns per-env state in HBM (SoA, env innermost) and launches the step/reset kernels
+// on the caller's stream.  No allocation, copy or synchronisation happens inside
+// wab_step / wab_reset / wab_rollout, so they are safe to capture in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wab.h"
+#include "wab_params.h"
+
+namespace wab {
+template <int MODE, int SLOTS>
+__global__ void wab_kernel(Params p);
+}
+
+using wab::Params;
+
+struct wab_handle {
+  Params p;
+  int device = 0;
+  int slots = 8;
+  int n_blocks = 0;
+  size_t lds_bytes = 0;
+  bool reset_done = false;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return fail(WAB_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+int n_actions_of(const wab_config* c) { return (c->gatherer_only || c->lookout_only) ? 5 : 6; }
+
+// masks wab_env.py:109-139 as 11-bit row masks (bit j <=> mask[i][j] == 1)
+const char* kLookout[11] = {"11100000111", "11000000011", "10000000001", "00000000000",
+                            "00000000000", "00000000000", "00000000000", "00000000000",
+                            "10000000001", "11000000011", "11100000111"};
+const char* kGatherer[11] = {"11111111111", "11111111111", "11111111111", "11110001111",
+                             "11100000111", "11100000111", "11100000111", "11110001111",
+                             "11111111111", "11111111111", "11111111111"};
+
+uint32_t row_mask(const char* s) {
+  uint32_t m = 0;
+  for (int j = 0; j < 11; ++j)
+    if (s[j] == '1') m |= 1u << j;
+  return m;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+template <int MODE>
+void* kernel_ptr(int slots) {
+  switch (slots) {
+    case 8: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 8>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 16>);
+    default: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 32>);
+  }
+}
+
+template <int MODE>
+int launch(wab_handle* h, const Params& p, hipStream_t stream) {
+  if (h->n_blocks == 0) return WAB_OK;
+  const dim3 grid(h->n_blocks), block(wab::kThreads);
+  switch (h->slots) {
+    case 8: hipLaunchKernelGGL((wab::wab_kernel<MODE, 8>), grid, block, h->lds_bytes, stream, p); break;
+    case 16: hipLaunchKernelGGL((wab::wab_kernel<MODE, 16>), grid, block, h->lds_bytes, stream, p); break;
+    default: hipLaunchKernelGGL((wab::wab_kernel<MODE, 32>), grid, block, h->lds_bytes, stream, p); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+
+bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+int check_obs(const wab_obs* o, const char* what) {
+  if (!o || !o->planes || !o->food_turns || !o->role || !o->status)
+    return fail(WAB_E_INVALID, std::string(what) + ": every wab_obs pointer must be set");
+  if (!aligned16(o->planes)) return fail(WAB_E_INVALID, std::string(what) + ": planes must be 16-byte aligned");
+  return WAB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wab_abi_version(void) { return WAB_ABI_VERSION; }
+
+const char* wab_last_error(void) { return g_err.c_str(); }
+
+int wab_num_actions(const wab_config* cfg) { return cfg ? n_actions_of(cfg) : WAB_E_INVALID; }
+
+int64_t wab_batch(const wab_handle* h) { return h ? h->p.B : 0; }
+
+int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id_base, int device,
+               wab_handle** out) {
+  g_err.clear();
+  if (!c || !out) return fail(WAB_E_INVALID, "wab_create: NULL argument");
+  *out = nullptr;
+  // --- validation (wab_env.py:147-148 and the limits of this implementation)
+  if (c->width % 2 == 0 || c->height % 2 == 0)
+    return fail(WAB_E_INVALID, "width and height must be odd numbers");
+  if (c->width < 1 || c->height < 1 || c->width > WAB_MAX_VIEW || c->height > WAB_MAX_VIEW)
+    return fail(WAB_E_INVALID, "width/height out of range [1, 63]");
+  if (c->restrict_view && (c->width < 11 || c->height < 11))
+    return fail(WAB_E_INVALID, "restrict_view needs width, height >= 11 (11x11 masks, wab_env.py:354)");
+  if (c->max_berries_per_bush < 0 || c->max_berries_per_bush > 255)
+    return fail(WAB_E_INVALID, "max_berries_per_bush must be in [0, 255]");
+  if (c->max_berries_per_bush > 0 && !c->bush_thresholds)
+    return fail(WAB_E_INVALID, "bush_thresholds is required");
+  if (c->turns_to_fill_food <= 0 || c->turns_to_empty_food <= 0)
+    return fail(WAB_E_INVALID, "turns_to_fill_food / turns_to_empty_food must be > 0");
+  if (c->turns_to_empty_food > 255) return fail(WAB_E_INVALID, "turns_to_empty_food must be <= 255 (u8 obs)");
+  if (c->wolf_spawn_margin < 0 || c->width / 2 + c->wolf_spawn_margin > 120 ||
+      c->height / 2 + c->wolf_spawn_margin > 120)
+    return fail(WAB_E_INVALID, "wolf_spawn_margin out of range");
+  const int slots = c->wolf_slots == 0 ? 8 : c->wolf_slots;
+  if (slots != 8 && slots != 16 && slots != 32) return fail(WAB_E_INVALID, "wolf_slots must be 8, 16 or 32");
+  const int S = c->plane_stride > 0 ? c->plane_stride : c->height;
+  if (S < c->height || S > 64) return fail(WAB_E_INVALID, "plane_stride must be in [height, 64]");
+  const int cap = c->eaten_capacity > 0 ? c->eaten_capacity : (c->max_turns > 0 ? c->max_turns : 1);
+  if (cap > 65535) return fail(WAB_E_INVALID, "eaten_capacity must be <= 65535");
+  if (batch < 0) return fail(WAB_E_INVALID, "batch must be >= 0");
+
+  wab_handle* h = new wab_handle();
+  Params& p = h->p;
+  std::memset(&p, 0, sizeof(p));
+  p.W = c->width;
+  p.H = c->height;
+  p.S = S;
+  p.cw = c->width / 2;
+  p.ch = c->height / 2;
+  p.margin = c->wolves ? c->wolf_spawn_margin : 0;
+  p.OB = 3 * p.W * p.S;
+  p.WH = p.W * p.H;
+  p.R = (p.W + 2 * p.margin) * (p.H + 2 * p.margin) - p.WH;
+  p.NT = p.WH + p.R;
+  p.RW = (p.R + 31) / 32;
+  p.WHW = (p.WH + 31) / 32;
+  p.magic_OB = (uint32_t)((1ull << 32) / (uint64_t)p.OB) + 1u;
+  p.n_actions = n_actions_of(c);
+  static const int dx[6] = {0, 1, 0, -1, 0, 0}, dy[6] = {1, 0, -1, 0, 0, 0};  // up right down left
+  for (int a = 0; a < 6; ++a) {
+    p.act_dx[a] = dx[a];
+    p.act_dy[a] = dy[a];
+    p.act_role[a] = -1;
+  }
+  if (c->gatherer_only) p.act_role[4] = 1;       // wab_env.py:149-159
+  else if (c->lookout_only) p.act_role[4] = 0;   // :160-170
+  else { p.act_role[4] = 1; p.act_role[5] = 0; } // :171-182
+  p.keep_gt = (uint64_t)std::floor(std::ldexp(c->wolf_chance_to_despawn, 53));       // u > p  (:263)
+  p.spawn_lt = (uint64_t)std::ceil(std::ldexp(c->chance_wolf_on_square / 2.0, 53));  // u < p/2 (:573)
+  p.max_berries = c->max_berries_per_bush;
+  p.bush_t1 = p.max_berries > 0 ? c->bush_thresholds[0] : (1ull << 53);
+  p.fill = 1.0 / (double)c->turns_to_fill_food;
+  p.hunger = 1.0 / (double)c->turns_to_empty_food;
+  p.r_turn = c->reward_per_turn;
+  p.r_killed = c->reward_for_being_killed;
+  p.r_starve = c->reward_for_starving;
+  p.r_finish = c->reward_for_finishing;
+  p.r_eat = c->reward_for_eating;
+  p.start_food = c->starting_food;
+  p.start_role = c->starting_role;
+  p.start_food_random = c->starting_food_random;
+  p.start_role_random = c->starting_role_random;
+  p.max_turns = c->max_turns;
+  p.turns_empty = c->turns_to_empty_food;
+  p.lookout_only = c->lookout_only;
+  p.restrict_view = c->restrict_view;
+  p.wolves_on = c->wolves;
+  p.wolves_can_move = c->wolves_can_move;
+  p.god_mode = c->god_mode;
+  p.autoreset = c->autoreset;
+  for (int i = 0; i < 11; ++i) {
+    p.mask_rows[0][i] = row_mask(kLookout[i]);
+    p.mask_rows[1][i] = row_mask(kGatherer[i]);
+  }
+  p.seed = seed;
+  p.env_base = env_id_base;
+  p.B = batch;
+  p.eaten_cap = cap;
+  h->device = device;
+  h->slots = slots;
+  h->n_blocks = (int)((batch + wab::kEnvsPerBlock - 1) / wab::kEnvsPerBlock);
+  h->lds_bytes = (size_t)wab::lds_layout(p, slots).total * 4u;
+  if (h->lds_bytes > 160u * 1024u) {
+    delete h;
+    return fail(WAB_E_INVALID, "viewport too large for the fused kernel's LDS budget");
+  }
+
+  DeviceGuard guard(device);
+  auto alloc = [&](void** ptr, size_t bytes) -> int {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(ptr, bytes);
+    if (e != hipSuccess) return fail(WAB_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    h->allocs.push_back(*ptr);
+    return WAB_OK;
+  };
+  const size_t B = (size_t)batch;
+  int rc = WAB_OK;
+  rc |= alloc((void**)&p.pos, B * 4);
+  rc |= alloc((void**)&p.food, B * 8);
+  rc |= alloc((void**)&p.turn, B * 4);
+  rc |= alloc((void**)&p.misc, B * 4);
+  rc |= alloc((void**)&p.episode, B * 4);
+  rc |= alloc((void**)&p.wolves, B * 4 * (size_t)slots);
+  rc |= alloc((void**)&p.eaten_xy, B * 4 * (size_t)cap);
+  rc |= alloc((void**)&p.eaten_rem, B * (size_t)cap);
+  rc |= alloc((void**)&p.counters, 4 * 8);
+  rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
+  uint64_t* thr = nullptr;
+  rc |= alloc((void**)&thr, (size_t)(p.max_berries > 0 ? p.max_berries : 1) * 8);
+  if (rc != WAB_OK) {
+    std::string msg = g_err;
+    wab_destroy(h);
+    return fail(WAB_E_NOMEM, msg);
+  }
+  p.thresholds = thr;
+  hipError_t e = hipSuccess;
+  if (p.max_berries > 0)
+    e = hipMemcpy(thr, c->bush_thresholds, (size_t)p.max_berries * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(p.episode, 0xFF, B * 4);
+  if (e == hipSuccess) e = hipMemset(p.misc, 0, B * 4);
+  if (e == hipSuccess) e = hipMemset(p.counters, 0, 4 * 8);
+  if (e == hipSuccess) e = hipMemset(p.block_resets, 0, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
+  for (void* k : {kernel_ptr<0>(slots), kernel_ptr<1>(slots)})
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    std::string msg = std::string("wab_create: ") + hipGetErrorString(e);
+    wab_destroy(h);
+    return fail(WAB_E_HIP, msg);
+  }
+  *out = h;
+  return WAB_OK;
+}
+
+int wab_destroy(wab_handle* h) {
+  if (!h) return WAB_OK;
+  {
+    DeviceGuard guard(h->device);
+    (void)hipDeviceSynchronize();
+    for (void* ptr : h->allocs) (void)hipFree(ptr);
+  }
+  delete h;
+  return WAB_OK;
+}
+
+int wab_reset(wab_handle* h, const uint8_t* mask, const wab_obs* obs, void* stream) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_reset: NULL handle");
+  if (int rc = check_obs(obs, "wab_reset")) return rc;
+  if (mask && !h->reset_done)
+    return fail(WAB_E_STATE, "wab_reset: the first reset must cover every env (mask = NULL)");
+  Params p = h->p;
+  p.reset_mask = mask;
+  p.planes = obs->planes;
+  p.food_turns = obs->food_turns;
+  p.role = obs->role;
+  p.status = obs->status;
+  DeviceGuard guard(h->device);
+  int rc = launch<1>(h, p, (hipStream_t)stream);
+  if (rc == WAB_OK && !mask) h->reset_done = true;
+  return rc;
+}
+
+int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward, uint8_t* done,
+             const wab_obs* terminal, void* stream) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_step: NULL handle");
+  if (!h->reset_done) return fail(WAB_E_STATE, "wab_step: call wab_reset before the first step");
+  if (!actions || !reward || !done) return fail(WAB_E_INVALID, "wab_step: NULL actions/reward/done");
+  if (int rc = check_obs(obs, "wab_step")) return rc;
+  Params p = h->p;
+  p.actions = actions;
+  p.planes = obs->planes;
+  p.food_turns = obs->food_turns;
+  p.role = obs->role;
+  p.status = obs->status;
+  p.reward = reward;
+  p.done = done;
+  if (terminal && terminal->planes) {
+    if (int rc = check_obs(terminal, "wab_step(terminal)")) return rc;
+    p.t_planes = terminal->planes;
+    p.t_food_turns = terminal->food_turns;
+    p.t_role = terminal->role;
+    p.t_status = terminal->status;
+  }
+  DeviceGuard guard(h->device);
+  return launch<0>(h, p, (hipStream_t)stream);
+}
+
+int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq, float* reward,
+                uint8_t* done, void* stream) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_rollout: NULL handle");
+  if (T < 0) return fail(WAB_E_INVALID, "wab_rollout: T must be >= 0");
+  if (int rc = check_obs(obs_seq, "wab_rollout")) return rc;
+  const int64_t B = h->p.B;
+  const size_t OB = (size_t)h->p.OB;
+  for (int32_t t = 0; t < T; ++t) {
+    wab_obs o;
+    o.planes = obs_seq->planes + (size_t)t * (size_t)B * OB;
+    o.food_turns = obs_seq->food_turns + (size_t)t * (size_t)B;
+    o.role = obs_seq->role + (size_t)t * (size_t)B;
+    o.status = obs_seq->status + (size_t)t * (size_t)B;
+    int rc = wab_step(h, actions + (size_t)t * (size_t)B, &o, reward + (size_t)t * (size_t)B,
+                      done + (size_t)t * (size_t)B, nullptr, stream);
+    if (rc != WAB_OK) return rc;
+  }
+  return WAB_OK;
+}
+
+int wab_get_counters(wab_handle* h, wab_counters* out, void* stream) {
+  g_err.clear();
+  if (!h || !out) return fail(WAB_E_INVALID, "wab_get_counters: NULL argument");
+  DeviceGuard guard(h->device);
+  unsigned long long c[4] = {0, 0, 0, 0};
+  std::vector<unsigned long long> br((size_t)(h->n_blocks > 0 ? h->n_blocks : 1));
+  HIP_TRY(hipMemcpyAsync(c, h->p.counters, sizeof(c), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipMemcpyAsync(br.data(), h->p.block_resets, br.size() * 8, hipMemcpyDeviceToHost,
+                         (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  out->wolf_overflow = c[0];
+  out->eaten_overflow = c[1];
+  out->bad_actions = c[2];
+  out->steps = 0;
+  out->resets = 0;
+  for (size_t i = 0; i < br.size(); ++i) out->resets += br[i];
+  return WAB_OK;
+}
+
+int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* turn, int32_t* n_wolves,
+                  uint32_t* episode, void* stream) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_get_state: NULL handle");
+  DeviceGuard guard(h->device);
+  const size_t B = (size_t)h->p.B;
+  std::vector<uint32_t> pos(B), misc(B);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(pos.data(), h->p.pos, B * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(misc.data(), h->p.misc, B * 4, hipMemcpyDeviceToHost, s));
+  if (food) HIP_TRY(hipMemcpyAsync(food, h->p.food, B * 8, hipMemcpyDeviceToHost, s));
+  if (turn) HIP_TRY(hipMemcpyAsync(turn, h->p.turn, B * 4, hipMemcpyDeviceToHost, s));
+  if (episode) HIP_TRY(hipMemcpyAsync(episode, h->p.episode, B * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (size_t i = 0; i < B; ++i) {
+    if (x) x[i] = wab::xy_x(pos[i]);
+    if (y) y[i] = wab::xy_y(pos[i]);
+    if (n_wolves) n_wolves[i] = (int32_t)((misc[i] >> 10) & 63u);
+  }
+  return WAB_OK;
+}
+
+}  // extern "C"

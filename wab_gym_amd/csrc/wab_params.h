@@ -1,0 +1,107 @@
+// wab_params.h — kernel parameter block shared by the C-ABI host code and the HIP kernels.
+//
+// Everything the fused step needs, resolved once at wab_create from wab_config
+// (include/wab.h) and passed by value as the kernel argument (scalar-loaded).
+#pragma once
+
+#include <stdint.h>
+
+namespace wab {
+
+constexpr int kEnvsPerBlock = 64;   // env lanes = wave 0 of the block
+constexpr int kThreads = 256;       // 4 waves: waves 0..3 share the tile-parallel phases
+constexpr int kMaxWolfSlots = 32;
+
+// per-env packed misc word: role [0,8) status [8,10) n_wolves [10,16) n_eaten [16,32)
+__host__ __device__ inline uint32_t misc_pack(uint32_t role, uint32_t status, uint32_t nw, uint32_t ne) {
+  return (role & 0xFFu) | ((status & 3u) << 8) | ((nw & 63u) << 10) | (ne << 16);
+}
+
+// tiles are packed (x & 0xFFFF) | (y << 16) with x, y int16 (absolute world coordinates)
+__host__ __device__ inline uint32_t xy_pack(int32_t x, int32_t y) {
+  return ((uint32_t)x & 0xFFFFu) | ((uint32_t)y << 16);
+}
+__host__ __device__ inline int32_t xy_x(uint32_t p) { return (int32_t)(int16_t)(p & 0xFFFFu); }
+__host__ __device__ inline int32_t xy_y(uint32_t p) { return (int32_t)(int16_t)(p >> 16); }
+
+struct Params {
+  // ---- geometry
+  int32_t W, H, S;          // viewport width (axis 0), height (axis 1), row stride in bytes
+  int32_t cw, ch, margin;   // W/2, H/2, wolf_spawn_margin
+  int32_t OB;               // obs bytes per env = 3*W*S (also obs bits per env in the LDS stream)
+  int32_t WH, R, NT;        // bush tiles, ring tiles, WH + R
+  int32_t RW, WHW;          // dwords of a ring mask / of a WH mask
+  uint32_t magic_OB;        // floor(2^32 / OB) + 1 (division helper)
+  // ---- rules
+  int32_t n_actions;
+  int32_t act_dx[6], act_dy[6], act_role[6];  // role -1 = NaN (unchanged)
+  uint64_t keep_gt;         // despawn: wolf kept iff U > keep_gt
+  uint64_t spawn_lt;        // spawn: wolf iff U < spawn_lt
+  uint64_t bush_t1;         // bush present iff U >= bush_t1 (2^53: never)
+  const uint64_t* thresholds;  // device [max_berries] T_k
+  int32_t max_berries;
+  double fill, hunger;
+  double r_turn, r_killed, r_starve, r_finish, r_eat;
+  double start_food;
+  int32_t start_role, start_food_random, start_role_random;
+  int32_t max_turns, turns_empty;
+  int32_t lookout_only, restrict_view, wolves_on, wolves_can_move, god_mode, autoreset;
+  uint32_t mask_rows[2][11];  // restrict_view: 11-bit row masks per role (bit j <=> mask[i][j])
+  // ---- identity
+  uint64_t seed;
+  int64_t env_base;
+  int64_t B;
+  int32_t eaten_cap;
+  // ---- state (device, SoA, env innermost)
+  uint32_t* pos;       // [B] packed ostrich tile
+  double* food;        // [B]
+  int32_t* turn;       // [B]
+  uint32_t* misc;      // [B]
+  uint32_t* episode;   // [B] current episode (0xFFFFFFFF before the first reset)
+  uint32_t* wolves;    // [slots][B] packed tiles
+  uint32_t* eaten_xy;  // [cap][B] packed tiles
+  uint8_t* eaten_rem;  // [cap][B] berries left
+  unsigned long long* counters;      // [3]: wolf_overflow, eaten_overflow, bad_actions (rare: atomics)
+  unsigned long long* block_resets;  // [n_blocks]: resets done by each block (owned, no atomics)
+  // ---- io (device, caller-owned)
+  const int8_t* actions;
+  const uint8_t* reset_mask;
+  uint8_t* planes;
+  uint8_t* food_turns;
+  uint8_t* role;
+  uint8_t* status;
+  float* reward;
+  uint8_t* done;
+  uint8_t* t_planes;   // terminal obs (nullable)
+  uint8_t* t_food_turns;
+  uint8_t* t_role;
+  uint8_t* t_status;
+};
+
+// LDS carve of one workgroup (dword offsets, each region 16-byte aligned).
+struct LdsLayout {
+  uint32_t sA, sB, spawnM, wolfM, tiles, snap, wl, jobEnv, jobKey, blk, total;
+};
+
+__host__ __device__ inline uint32_t lds_align4(uint32_t n) { return (n + 3u) & ~3u; }
+
+__host__ __device__ inline LdsLayout lds_layout(const Params& p, int slots) {
+  const uint32_t NE = (uint32_t)kEnvsPerBlock;
+  const uint32_t streamW = (NE * (uint32_t)p.OB) >> 5;
+  LdsLayout L;
+  uint32_t o = 0;
+  L.sA = o; o += lds_align4(streamW);
+  L.sB = o; o += lds_align4(streamW);
+  L.spawnM = o; o += lds_align4(NE * (uint32_t)p.RW);
+  L.wolfM = o; o += lds_align4(NE * (uint32_t)p.WHW);
+  L.tiles = o; o += lds_align4((uint32_t)p.NT);
+  L.snap = o; o += NE * 4u;
+  L.wl = o; o += lds_align4(NE * (uint32_t)slots);
+  L.jobEnv = o; o += NE;
+  L.jobKey = o; o += 2u * NE;
+  L.blk = o; o += 4u;
+  L.total = o;
+  return L;
+}
+
+}  // namespace wab

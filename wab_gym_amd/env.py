@@ -1,0 +1,202 @@
+"""BatchedWolvesAndBushesEnv — the reference's gym surface with a leading batch dimension.
+
+Mirrors `WolvesAndBushesEnv` (wab_env.py:103-342): same constructor options
+(`game_options`, validated like wab_env.py:147-148), `reset()`, `step(actions)` ->
+`(obs, reward, done, info)`, `action_space`, `observation_space`, `spec`.  Every call
+advances `num_envs` independent envs at once through one fused HIP kernel (C-ABI in
+include/wab.h).  Buffers are PyTorch-ROCm tensors on the env's device.
+
+Observation: the reference's 7-tuple (wab_env.py:374-385) batched:
+    (wolf_grid [B,W,H] u8, bush_grid [B,W,H] u8, ostrich_grid [B,W,H] u8,
+     food_turns [B] u8, role [B] u8, alive_starved_killed [B] u8, view_mask [B,11,11] u8)
+The grids are views into an env-owned buffer that the next call overwrites (clone to keep).
+
+Differences from the reference, by design (documented in DESIGN.md):
+  * random draws are keyed by (seed, env id, episode, what is drawn) instead of numpy's
+    global MT19937 stream, so batches are reproducible and shard-invariant;
+  * with `autoreset=True` (default) an env whose step returns done=True is reset inside
+    the same call; `obs` then holds the new episode's first observation and
+    `info["terminal_obs"]` (if `return_terminal=True`) the step's own observation;
+  * an action outside [0, n_actions) raises IndexError (the reference raises for
+    a >= n via `.iloc` and silently wraps negatives, wab_env.py:253).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .options import default_game_options, make_config, n_actions, view_masks
+from .spaces import Box, Discrete, DummySpec, Tuple
+
+
+class BatchedWolvesAndBushesEnv:
+    metadata = {"render.modes": ["rgb_array"], "video.frames_per_second": 12}
+
+    def __init__(self, game_options=None, num_envs=4096, seed=0x5EED, device="cuda",
+                 env_id_base=0, autoreset=True, return_terminal=False, plane_stride=0,
+                 wolf_slots=0, eaten_capacity=0, validate_actions=True):
+        import torch
+
+        self._torch = torch
+        lib = _lib.load()
+        opts = dict(default_game_options if game_options is None else game_options)
+        for k, v in default_game_options.items():
+            opts.setdefault(k, v)
+        self.game_options = opts
+        self.cfg, self._keep = make_config(opts, autoreset=autoreset, plane_stride=plane_stride,
+                                           eaten_capacity=eaten_capacity, wolf_slots=wolf_slots)
+        self.num_envs = int(num_envs)
+        self.base_seed = int(seed)
+        self.env_id_base = int(env_id_base)
+        self.autoreset = bool(autoreset)
+        self.return_terminal = bool(return_terminal)
+        self.validate_actions = bool(validate_actions)
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("BatchedWolvesAndBushesEnv runs on a HIP device (device='cuda[:i]')")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.W, self.H = self.cfg.width, self.cfg.height
+        self.S = plane_stride or self.H
+        h = ctypes.c_void_p()
+        _lib.check(lib.wab_create(ctypes.addressof(self.cfg), self.num_envs, self.base_seed,
+                                  self.env_id_base, dev.index, ctypes.byref(h)), "wab_create")
+        self._h = h
+        B = self.num_envs
+        u8 = dict(dtype=torch.uint8, device=dev)
+        self._obs = self._alloc_obs()
+        self._term = self._alloc_obs() if self.return_terminal else None
+        self.reward = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(B, **u8)
+        self._actions = torch.zeros(B, dtype=torch.int8, device=dev)
+        self._masks = torch.as_tensor(view_masks(opts), device=dev)
+        self._zero_mask = torch.zeros((11, 11), **u8)
+        self._reset_once = False
+        self.n_actions = n_actions(opts)
+        self.action_space = Discrete(self.n_actions)  # wab_env.py:188-191
+        W, H = self.W, self.H
+        self.single_observation_space = Tuple((        # wab_env.py:193-229
+            Box(0, 1, (W, H)), Box(0, 1, (W, H)), Box(0, 1, (W, H)),
+            Discrete(opts["turns_to_empty_food"] + 1), Discrete(2), Discrete(3)))
+        self.observation_space = Tuple((
+            Box(0, 1, (B, W, H)), Box(0, 1, (B, W, H)), Box(0, 1, (B, W, H)),
+            Box(0, opts["turns_to_empty_food"], (B,)), Box(0, 1, (B,)), Box(0, 2, (B,))))
+        self.spec = DummySpec(id="WolvesAndBushes-v0", max_episode_steps=opts["max_turns"],
+                              reward_threshold=80)  # wab_env.py:140-146
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc_obs(self):
+        t = self._torch
+        B = self.num_envs
+        planes = t.zeros((B, 3, self.W, self.S), dtype=t.uint8, device=self.device)
+        scal = t.zeros((3, B), dtype=t.uint8, device=self.device)
+        st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr())
+        return {"planes": planes, "scalars": scal, "struct": st}
+
+    def _obs_tuple(self, o):
+        planes, scal = o["planes"], o["scalars"]
+        H = self.H
+        grids = [planes[:, k, :, :H] for k in range(3)]
+        if self.game_options["restrict_view"]:
+            vm = self._masks[scal[1].long()]
+        else:
+            vm = self._zero_mask.expand(self.num_envs, 11, 11)
+        return (grids[0], grids[1], grids[2], scal[0], scal[1], scal[2], vm)
+
+    def _stream(self):
+        return ctypes.c_void_p(self._torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ gym surface
+    def reset(self, mask=None):
+        """Reset all envs (mask=None) or those with mask[i] true; returns the batched obs."""
+        t = self._torch
+        m = None
+        if mask is not None:
+            if not self._reset_once:
+                raise RuntimeError("the first reset must cover every env (mask=None)")
+            m = t.as_tensor(mask, device=self.device).to(t.uint8).contiguous()
+            if m.shape != (self.num_envs,):
+                raise ValueError("mask must have shape [num_envs]")
+        _lib.check(_lib.load().wab_reset(self._h, None if m is None else m.data_ptr(),
+                                         ctypes.addressof(self._obs["struct"]), self._stream()),
+                   "wab_reset")
+        self._reset_mask_keepalive = m
+        self._reset_once = True
+        return self._obs_tuple(self._obs)
+
+    def step(self, actions):
+        """Advance every env one step (wab_env.py:250-342)."""
+        t = self._torch
+        if not self._reset_once:
+            raise RuntimeError("call reset() before step()")
+        a = t.as_tensor(actions, device=self.device)
+        if a.shape != (self.num_envs,):
+            raise ValueError("actions must have shape [num_envs]")
+        if self.validate_actions:
+            if bool(((a < 0) | (a >= self.n_actions)).any()):
+                raise IndexError("action out of range [0, %d)" % self.n_actions)
+        if a.dtype != t.int8:
+            self._actions.copy_(a)
+            a = self._actions
+        else:
+            a = a.contiguous()
+        term = ctypes.addressof(self._term["struct"]) if self._term is not None else None
+        _lib.check(_lib.load().wab_step(self._h, a.data_ptr(), ctypes.addressof(self._obs["struct"]),
+                                        self.reward.data_ptr(), self.done.data_ptr(), term,
+                                        self._stream()), "wab_step")
+        info = {}
+        if self._term is not None:
+            info["terminal_obs"] = self._obs_tuple(self._term)
+        return self._obs_tuple(self._obs), self.reward, self.done.bool(), info
+
+    def rollout(self, actions):
+        """T fused steps: actions [T, B] -> (planes [T,B,3,W,S], scalars [T,3,B], reward [T,B],
+        done [T,B]).  Equivalent to T step() calls without terminal observations."""
+        t = self._torch
+        a = t.as_tensor(actions, device=self.device).to(t.int8).contiguous()
+        T = a.shape[0]
+        planes = t.empty((T, self.num_envs, 3, self.W, self.S), dtype=t.uint8, device=self.device)
+        scal = t.empty((3, T, self.num_envs), dtype=t.uint8, device=self.device)
+        rew = t.empty((T, self.num_envs), dtype=t.float32, device=self.device)
+        done = t.empty((T, self.num_envs), dtype=t.uint8, device=self.device)
+        o = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr())
+        _lib.check(_lib.load().wab_rollout(self._h, a.data_ptr(), T, ctypes.addressof(o),
+                                           rew.data_ptr(), done.data_ptr(), self._stream()),
+                   "wab_rollout")
+        return planes, scal.permute(1, 0, 2), rew, done
+
+    def counters(self):
+        c = _lib.WabCounters()
+        _lib.check(_lib.load().wab_get_counters(self._h, ctypes.addressof(c), self._stream()),
+                   "wab_get_counters")
+        return {k: int(getattr(c, k)) for k, _ in _lib.WabCounters._fields_}
+
+    def state(self):
+        """Hidden per-env state (host numpy): food f64, x, y, turn, n_wolves, episode."""
+        B = self.num_envs
+        food = np.zeros(B, np.float64)
+        x, y, turn, nw = (np.zeros(B, np.int32) for _ in range(4))
+        ep = np.zeros(B, np.uint32)
+        P = lambda a: a.ctypes.data  # noqa: E731
+        _lib.check(_lib.load().wab_get_state(self._h, P(food), P(x), P(y), P(turn), P(nw), P(ep),
+                                             self._stream()), "wab_get_state")
+        return dict(food=food, x=x, y=y, turn=turn, n_wolves=nw, episode=ep)
+
+    def seed(self, seed=None):
+        """No-op like gym 0.17's Env.seed in the reference (wab_env.py:1014); draws are keyed
+        by the constructor's `seed`."""
+        return [self.base_seed]
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().wab_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
