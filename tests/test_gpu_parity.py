@@ -38,10 +38,11 @@ def test_gpu_golden_8_slots_and_padded_stride():
 
 # ------------------------------------------------------------------ lockstep vs oracle
 def _lockstep(opts, n, T, autoreset=True, stride=0, threads=16, seed_actions=0, base=0,
-              check_terminal=True):
+              check_terminal=True, wolf_slots=0):
     import torch
 
-    env = _env(opts, n, base, autoreset=autoreset, return_terminal=True, plane_stride=stride)
+    env = _env(opts, n, base, autoreset=autoreset, return_terminal=True, plane_stride=stride,
+               wolf_slots=wolf_slots)
     orc = _oracle(opts, n, base, autoreset, stride)
     obs = env.reset()
     op, of, orl, ost = orc.reset()
@@ -99,7 +100,7 @@ def test_option_variants_lockstep():
                  {"wolves": False}, {"wolves_can_move": False, "god_mode": True},
                  {"starting_food": None, "starting_role": None}, {"width": 9, "height": 13},
                  {"width": 1, "height": 3}, {"width": 45, "height": 45}):
-        _lockstep(opts, 640, 90, base=77)
+        _lockstep(opts, 640, 90, base=77, wolf_slots=32)  # 45x45 exceeds 8 live wolves
 
 
 def test_partial_batch_and_large_env_ids():
@@ -192,7 +193,7 @@ def test_full_size_properties():
         assert bool(((obs[0] <= 1) & (obs[1] <= 1)).all())
         total_done += int(done.sum())
     c = env.counters()
-    assert c["resets"] == total_done
+    assert c["resets"] == total_done + 65536  # + the initial reset of every env
     assert c["wolf_overflow"] == 0 and c["eaten_overflow"] == 0
     # mean episode length of a random policy ~41 steps
     assert 30 < 65536 * 200 / max(total_done, 1) < 55
