@@ -75,7 +75,8 @@ typedef struct wab_config {
   /* ---- batched-surface extensions ---- */
   int32_t autoreset;               /* 1: a done env is reset inside the same step call */
   int32_t plane_stride;            /* bytes per grid row in `planes` (>= height; 0 = height) */
-  int32_t eaten_capacity;          /* eaten-tile log slots per env (0 = max(max_turns, 1)) */
+  int32_t eaten_capacity;          /* eaten-tile log slots per env, <= 255
+                                    * (0 = max_turns clamped to [1, 255]) */
   int32_t wolf_slots;              /* live-wolf slots per env: 8 (0 = 8), 16 or 32; a spawn
                                     * beyond them is dropped and counted (wolf_overflow) */
   /* T_k (k = 1..max_berries_per_bush): the smallest 53-bit U with

@@ -26,6 +26,12 @@ def _has_gpu():
 
 def pytest_collection_modifyitems(config, items):
     has_ref = os.path.isdir(os.environ.get("WAB_REFERENCE", "/root/reference"))
+    gpu = None
     for item in items:
         if "reference" in item.keywords and not has_ref:
             item.add_marker(pytest.mark.skip(reason="reference not mounted"))
+        if "gpu" in item.keywords:
+            if gpu is None:
+                gpu = _has_gpu()
+            if not gpu:
+                item.add_marker(pytest.mark.skip(reason="no HIP device in this container"))

@@ -1,0 +1,80 @@
+"""Diagnostic: per-phase time of the fused step kernel from in-kernel s_memrealtime stamps.
+
+Builds a separate -DWAB_STAMPS library (never the product build), runs B envs for a few
+hundred steps and prints the mean duration of each phase boundary interval over blocks,
+plus the launch span (first block start -> last block end).  Shares only; the stamps
+themselves cost time.  Usage (GPU box): python tools/phase_stamps.py [--batch 65536] [--config default]
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+OUT = os.path.join(REPO, "wab_gym_amd", "_lib", "libwab_hip_stamps.so")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--config", default="default")
+    args = ap.parse_args()
+    import __graft_entry__ as ge
+
+    src = [os.path.join(ge.CSRC, s) for s in ge.HIP_SOURCES]
+    subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS", "-o", OUT] + src, check=True)
+    os.environ["WAB_LIB"] = OUT
+    import numpy as np
+    import torch
+
+    import bench
+    from wab_gym_amd import _lib
+    from wab_gym_amd.env import BatchedWolvesAndBushesEnv
+
+    opts, stride, _ = bench.CONFIGS[args.config]
+    B = args.batch
+    env = BatchedWolvesAndBushesEnv(opts, num_envs=B, device="cuda:0", validate_actions=False,
+                                    plane_stride=stride)
+    L = _lib.load()
+    L.wab_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    nb = (B + 63) // 64
+    st = torch.zeros((nb, 16), dtype=torch.int64, device="cuda:0")
+    env.reset()
+    L.wab_debug_set_stamps(env._h, st.data_ptr())
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0)
+    acc, spans = [], []
+    sub_acc = {k: [] for k in [(3, 7), (7, 8), (8, 9), (9, 10), (10, 11), (11, 12), (12, 4)]}
+    for t in range(args.steps):
+        st.zero_()
+        env.step(torch.randint(0, env.n_actions, (B,), device="cuda:0", generator=g))
+        torch.cuda.synchronize()
+        if t < 20:
+            continue
+        s = st.cpu().numpy().astype(np.int64)
+        d = np.diff(s[:, :7], axis=1)  # phase intervals per block (10 ns ticks)
+        acc.append(d.mean(axis=0))
+        spans.append(s[:, 6].max() - s[:, 0].min())
+        for (a0, a1) in sub_acc:
+            sub_acc[(a0, a1)].append((s[:, a1] - s[:, a0]).mean())
+    a = np.mean(acc, axis=0) * 10 / 1000
+    names = ["A: loads+LDS init", "A2: bitmap scroll", "B: keyed draws", "C: dynamics+stores",
+             "D/E: reset jobs", "F: expand+store"]
+    for n, v in zip(names, a):
+        print("%-22s %7.2f us" % (n, v))
+    print("%-22s %7.2f us (sum of block means)" % ("block total", a.sum()))
+    print("%-22s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
+    # phase C detail: 3 -> 7 -> 8 -> 9 -> 10 -> 11 -> 12 -> 4
+    sub = [("C1: log scan", 3, 7), ("C2: bitmap->plane", 7, 8), ("C3: wolves", 8, 9),
+           ("C4: eat", 9, 10), ("C5: starve+spawn", 10, 11), ("C6: reward", 11, 12),
+           ("C7: jobs+stores", 12, 4)]
+    for n, a0, a1 in sub:
+        v = np.mean(sub_acc[(a0, a1)]) * 10 / 1000
+        print("  %-20s %7.2f us" % (n, v))
+
+
+if __name__ == "__main__":
+    main()

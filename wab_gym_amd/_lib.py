@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libwab_hip.so")
+LIB_PATH = os.environ.get("WAB_LIB") or os.path.join(HERE, "_lib", "libwab_hip.so")
 
 EXPORTED = [
     "wab_abi_version", "wab_last_error", "wab_num_actions", "wab_create", "wab_destroy",

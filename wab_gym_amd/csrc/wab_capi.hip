@@ -15,7 +15,7 @@
 #include "wab_params.h"
 
 namespace wab {
-template <int MODE, int SLOTS>
+template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
 }
 
@@ -76,26 +76,46 @@ struct DeviceGuard {
   }
 };
 
-template <int MODE>
+template <int MODE, bool SMALL>
 void* kernel_ptr(int slots) {
   switch (slots) {
-    case 8: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 8>);
-    case 16: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 16>);
-    default: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 32>);
+    case 8: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 8, SMALL>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 16, SMALL>);
+    default: return reinterpret_cast<void*>(&wab::wab_kernel<MODE, 32, SMALL>);
   }
 }
+
+template <int MODE, bool SMALL>
+void launch_as(wab_handle* h, const Params& p, hipStream_t stream) {
+  const dim3 grid(h->n_blocks), block(wab::kThreads);
+  switch (h->slots) {
+    case 8: hipLaunchKernelGGL((wab::wab_kernel<MODE, 8, SMALL>), grid, block, h->lds_bytes, stream, p); break;
+    case 16: hipLaunchKernelGGL((wab::wab_kernel<MODE, 16, SMALL>), grid, block, h->lds_bytes, stream, p); break;
+    default: hipLaunchKernelGGL((wab::wab_kernel<MODE, 32, SMALL>), grid, block, h->lds_bytes, stream, p); break;
+  }
+}
+
+// SMALL: the W*H-bit view bitmap fits 4 registers (default 11x11 = 121 bits)
+bool small_map(const Params& p) { return p.WHW <= 4; }
 
 template <int MODE>
 int launch(wab_handle* h, const Params& p, hipStream_t stream) {
   if (h->n_blocks == 0) return WAB_OK;
-  const dim3 grid(h->n_blocks), block(wab::kThreads);
-  switch (h->slots) {
-    case 8: hipLaunchKernelGGL((wab::wab_kernel<MODE, 8>), grid, block, h->lds_bytes, stream, p); break;
-    case 16: hipLaunchKernelGGL((wab::wab_kernel<MODE, 16>), grid, block, h->lds_bytes, stream, p); break;
-    default: hipLaunchKernelGGL((wab::wab_kernel<MODE, 32>), grid, block, h->lds_bytes, stream, p); break;
-  }
+  if (small_map(p)) launch_as<MODE, true>(h, p, stream);
+  else launch_as<MODE, false>(h, p, stream);
   HIP_TRY(hipGetLastError());
   return WAB_OK;
+}
+
+// "U >= T" with U = hi << 21 | lo21 becomes (hi, lo21) >= (th, tl); T >= 2^53 never holds
+void split_threshold(uint64_t T, uint32_t* th, uint32_t* tl) {
+  if (T >= (1ull << 53)) {
+    *th = 0xFFFFFFFFu;
+    *tl = 0xFFFFFFFFu;
+  } else {
+    *th = (uint32_t)(T >> 21);
+    *tl = (uint32_t)(T & 0x1FFFFFu);
+  }
 }
 
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -145,8 +165,9 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   if (slots != 8 && slots != 16 && slots != 32) return fail(WAB_E_INVALID, "wolf_slots must be 8, 16 or 32");
   const int S = c->plane_stride > 0 ? c->plane_stride : c->height;
   if (S < c->height || S > 64) return fail(WAB_E_INVALID, "plane_stride must be in [height, 64]");
-  const int cap = c->eaten_capacity > 0 ? c->eaten_capacity : (c->max_turns > 0 ? c->max_turns : 1);
-  if (cap > 65535) return fail(WAB_E_INVALID, "eaten_capacity must be <= 65535");
+  const int cap = c->eaten_capacity > 0 ? c->eaten_capacity
+                                        : (c->max_turns < 1 ? 1 : (c->max_turns > 255 ? 255 : c->max_turns));
+  if (cap > 255) return fail(WAB_E_INVALID, "eaten_capacity must be <= 255");
   if (batch < 0) return fail(WAB_E_INVALID, "batch must be >= 0");
 
   wab_handle* h = new wab_handle();
@@ -164,6 +185,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   p.NT = p.WH + p.R;
   p.RW = (p.R + 31) / 32;
   p.WHW = (p.WH + 31) / 32;
+  p.SL = p.W > p.H ? p.W : p.H;
   p.magic_OB = (uint32_t)((1ull << 32) / (uint64_t)p.OB) + 1u;
   p.n_actions = n_actions_of(c);
   static const int dx[6] = {0, 1, 0, -1, 0, 0}, dy[6] = {1, 0, -1, 0, 0, 0};  // up right down left
@@ -175,10 +197,14 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   if (c->gatherer_only) p.act_role[4] = 1;       // wab_env.py:149-159
   else if (c->lookout_only) p.act_role[4] = 0;   // :160-170
   else { p.act_role[4] = 1; p.act_role[5] = 0; } // :171-182
-  p.keep_gt = (uint64_t)std::floor(std::ldexp(c->wolf_chance_to_despawn, 53));       // u > p  (:263)
-  p.spawn_lt = (uint64_t)std::ceil(std::ldexp(c->chance_wolf_on_square / 2.0, 53));  // u < p/2 (:573)
+  // thresholds on the 53-bit draw U (u = U * 2^-53), each as a ">= T" test
+  const uint64_t keep_ge = (uint64_t)std::floor(std::ldexp(c->wolf_chance_to_despawn, 53)) + 1;  // u > p (:263)
+  const uint64_t spawn_ge = (uint64_t)std::ceil(std::ldexp(c->chance_wolf_on_square / 2.0, 53));  // u < p/2 (:573)
   p.max_berries = c->max_berries_per_bush;
-  p.bush_t1 = p.max_berries > 0 ? c->bush_thresholds[0] : (1ull << 53);
+  const uint64_t bush_ge = p.max_berries > 0 ? c->bush_thresholds[0] : (1ull << 53);          // food > 0
+  split_threshold(keep_ge, &p.keep_th, &p.keep_tl);
+  split_threshold(spawn_ge, &p.spawn_th, &p.spawn_tl);
+  split_threshold(bush_ge, &p.bush_th, &p.bush_tl);
   p.fill = 1.0 / (double)c->turns_to_fill_food;
   p.hunger = 1.0 / (double)c->turns_to_empty_food;
   p.r_turn = c->reward_per_turn;
@@ -201,6 +227,12 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   for (int i = 0; i < 11; ++i) {
     p.mask_rows[0][i] = row_mask(kLookout[i]);
     p.mask_rows[1][i] = row_mask(kGatherer[i]);
+  }
+  for (int c = 0; c < p.WH && c < 128; ++c) {  // bitmap masks for W*H <= 128 (bit c = i*H + j)
+    const int j = c % p.H;
+    p.small_masks[2][c >> 5] |= 1u << (c & 31);
+    if (j == 0) p.small_masks[0][c >> 5] |= 1u << (c & 31);
+    if (j == p.H - 1) p.small_masks[1][c >> 5] |= 1u << (c & 31);
   }
   p.seed = seed;
   p.env_base = env_id_base;
@@ -225,14 +257,12 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   };
   const size_t B = (size_t)batch;
   int rc = WAB_OK;
-  rc |= alloc((void**)&p.pos, B * 4);
+  rc |= alloc((void**)&p.hdr, B * 16);
   rc |= alloc((void**)&p.food, B * 8);
-  rc |= alloc((void**)&p.turn, B * 4);
-  rc |= alloc((void**)&p.misc, B * 4);
-  rc |= alloc((void**)&p.episode, B * 4);
   rc |= alloc((void**)&p.wolves, B * 4 * (size_t)slots);
   rc |= alloc((void**)&p.eaten_xy, B * 4 * (size_t)cap);
   rc |= alloc((void**)&p.eaten_rem, B * (size_t)cap);
+  rc |= alloc((void**)&p.bushmap, B * 4 * (size_t)p.WHW);
   rc |= alloc((void**)&p.counters, 4 * 8);
   rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   uint64_t* thr = nullptr;
@@ -246,11 +276,14 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   hipError_t e = hipSuccess;
   if (p.max_berries > 0)
     e = hipMemcpy(thr, c->bush_thresholds, (size_t)p.max_berries * 8, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemset(p.episode, 0xFF, B * 4);
-  if (e == hipSuccess) e = hipMemset(p.misc, 0, B * 4);
+  if (e == hipSuccess && B > 0) {  // every env: episode 0xFFFFFFFF (the first reset makes it 0)
+    std::vector<uint4> init(B, make_uint4(0u, 0u, 0u, 0xFFFFFFFFu));
+    e = hipMemcpy(p.hdr, init.data(), B * 16, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemset(p.counters, 0, 4 * 8);
   if (e == hipSuccess) e = hipMemset(p.block_resets, 0, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
-  for (void* k : {kernel_ptr<0>(slots), kernel_ptr<1>(slots)})
+  for (void* k : {kernel_ptr<0, true>(slots), kernel_ptr<1, true>(slots), kernel_ptr<0, false>(slots),
+                  kernel_ptr<1, false>(slots)})
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -364,20 +397,28 @@ int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* 
   if (!h) return fail(WAB_E_INVALID, "wab_get_state: NULL handle");
   DeviceGuard guard(h->device);
   const size_t B = (size_t)h->p.B;
-  std::vector<uint32_t> pos(B), misc(B);
+  std::vector<uint4> hdr(B);
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemcpyAsync(pos.data(), h->p.pos, B * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(misc.data(), h->p.misc, B * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(hdr.data(), h->p.hdr, B * 16, hipMemcpyDeviceToHost, s));
   if (food) HIP_TRY(hipMemcpyAsync(food, h->p.food, B * 8, hipMemcpyDeviceToHost, s));
-  if (turn) HIP_TRY(hipMemcpyAsync(turn, h->p.turn, B * 4, hipMemcpyDeviceToHost, s));
-  if (episode) HIP_TRY(hipMemcpyAsync(episode, h->p.episode, B * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   for (size_t i = 0; i < B; ++i) {
-    if (x) x[i] = wab::xy_x(pos[i]);
-    if (y) y[i] = wab::xy_y(pos[i]);
-    if (n_wolves) n_wolves[i] = (int32_t)((misc[i] >> 10) & 63u);
+    if (x) x[i] = wab::xy_x(hdr[i].x);
+    if (y) y[i] = wab::xy_y(hdr[i].x);
+    if (turn) turn[i] = (int32_t)hdr[i].y;
+    if (n_wolves) n_wolves[i] = (int32_t)wab::misc_nw(hdr[i].z);
+    if (episode) episode[i] = hdr[i].w;
   }
   return WAB_OK;
 }
+
+#ifdef WAB_STAMPS
+// diagnostic build only: per-block phase timestamps (see wab_step.hip, WAB_STAMP)
+int wab_debug_set_stamps(wab_handle* h, unsigned long long* dev) {
+  if (!h) return WAB_E_INVALID;
+  h->p.stamps = dev;
+  return WAB_OK;
+}
+#endif
 
 }  // extern "C"

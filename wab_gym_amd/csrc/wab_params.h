@@ -12,10 +12,18 @@ constexpr int kEnvsPerBlock = 64;   // env lanes = wave 0 of the block
 constexpr int kThreads = 256;       // 4 waves: waves 0..3 share the tile-parallel phases
 constexpr int kMaxWolfSlots = 32;
 
-// per-env packed misc word: role [0,8) status [8,10) n_wolves [10,16) n_eaten [16,32)
-__host__ __device__ inline uint32_t misc_pack(uint32_t role, uint32_t status, uint32_t nw, uint32_t ne) {
-  return (role & 0xFFu) | ((status & 3u) << 8) | ((nw & 63u) << 10) | (ne << 16);
+// per-env packed misc word: role [0,8) status [8,10) n_wolves [10,16) n_eaten [16,24)
+// n_emptied [24,32) (eaten-log entries with no berries left)
+__host__ __device__ inline uint32_t misc_pack(uint32_t role, uint32_t status, uint32_t nw, uint32_t ne,
+                                              uint32_t ndep) {
+  return (role & 0xFFu) | ((status & 3u) << 8) | ((nw & 63u) << 10) | ((ne & 0xFFu) << 16) |
+         ((ndep & 0xFFu) << 24);
 }
+__host__ __device__ inline uint32_t misc_role(uint32_t m) { return m & 0xFFu; }
+__host__ __device__ inline uint32_t misc_status(uint32_t m) { return (m >> 8) & 3u; }
+__host__ __device__ inline uint32_t misc_nw(uint32_t m) { return (m >> 10) & 63u; }
+__host__ __device__ inline uint32_t misc_ne(uint32_t m) { return (m >> 16) & 0xFFu; }
+__host__ __device__ inline uint32_t misc_ndep(uint32_t m) { return m >> 24; }
 
 // tiles are packed (x & 0xFFFF) | (y << 16) with x, y int16 (absolute world coordinates)
 __host__ __device__ inline uint32_t xy_pack(int32_t x, int32_t y) {
@@ -30,14 +38,17 @@ struct Params {
   int32_t cw, ch, margin;   // W/2, H/2, wolf_spawn_margin
   int32_t OB;               // obs bytes per env = 3*W*S (also obs bits per env in the LDS stream)
   int32_t WH, R, NT;        // bush tiles, ring tiles, WH + R
-  int32_t RW, WHW;          // dwords of a ring mask / of a WH mask
+  int32_t RW, WHW;          // dwords of a ring mask / of a WH mask (WHW = bush bitmap words)
+  int32_t SL;               // strip slots per env = max(W, H) (tiles entering the view on a move)
   uint32_t magic_OB;        // floor(2^32 / OB) + 1 (division helper)
   // ---- rules
   int32_t n_actions;
   int32_t act_dx[6], act_dy[6], act_role[6];  // role -1 = NaN (unchanged)
-  uint64_t keep_gt;         // despawn: wolf kept iff U > keep_gt
-  uint64_t spawn_lt;        // spawn: wolf iff U < spawn_lt
-  uint64_t bush_t1;         // bush present iff U >= bush_t1 (2^53: never)
+  // "U >= T" tests on 53-bit draws U = hi << 21 | lo21, split as (T >> 21, T & 0x1FFFFF);
+  // T = 2^53 ("never") is encoded (0xFFFFFFFF, 0xFFFFFFFF) which no (hi, lo21) reaches
+  uint32_t keep_th, keep_tl;    // despawn: wolf kept iff U >= keep_gt + 1  (u > p, wab_env.py:263)
+  uint32_t spawn_th, spawn_tl;  // spawn: wolf iff !(U >= spawn_lt)          (u < p/2, wab_env.py:573)
+  uint32_t bush_th, bush_tl;    // bush present iff U >= T_1                 (wab_env.py:632-635)
   const uint64_t* thresholds;  // device [max_berries] T_k
   int32_t max_berries;
   double fill, hunger;
@@ -47,20 +58,19 @@ struct Params {
   int32_t max_turns, turns_empty;
   int32_t lookout_only, restrict_view, wolves_on, wolves_can_move, god_mode, autoreset;
   uint32_t mask_rows[2][11];  // restrict_view: 11-bit row masks per role (bit j <=> mask[i][j])
+  uint32_t small_masks[3][4]; // W*H <= 128: column 0, column H-1, valid-bit masks of the bitmap
   // ---- identity
   uint64_t seed;
   int64_t env_base;
   int64_t B;
   int32_t eaten_cap;
   // ---- state (device, SoA, env innermost)
-  uint32_t* pos;       // [B] packed ostrich tile
+  uint4* hdr;          // [B] {ostrich tile, turn, misc, episode (0xFFFFFFFF before the first reset)}
   double* food;        // [B]
-  int32_t* turn;       // [B]
-  uint32_t* misc;      // [B]
-  uint32_t* episode;   // [B] current episode (0xFFFFFFFF before the first reset)
   uint32_t* wolves;    // [slots][B] packed tiles
   uint32_t* eaten_xy;  // [cap][B] packed tiles
   uint8_t* eaten_rem;  // [cap][B] berries left
+  uint32_t* bushmap;   // [WHW][B] bush presence of the current view, bit i*H + j (post-eat)
   unsigned long long* counters;      // [3]: wolf_overflow, eaten_overflow, bad_actions (rare: atomics)
   unsigned long long* block_resets;  // [n_blocks]: resets done by each block (owned, no atomics)
   // ---- io (device, caller-owned)
@@ -76,16 +86,17 @@ struct Params {
   uint8_t* t_food_turns;
   uint8_t* t_role;
   uint8_t* t_status;
+  unsigned long long* stamps;  // diagnostic builds only (-DWAB_STAMPS): [n_blocks][16] s_memrealtime
 };
 
 // LDS carve of one workgroup (dword offsets, each region 16-byte aligned).
 struct LdsLayout {
-  uint32_t sA, sB, spawnM, wolfM, tiles, snap, wl, jobEnv, jobKey, blk, total;
+  uint32_t sA, sB, spawnM, wolfM, bm, masks, tiles, snap, jobEnv, jobKey, blk, thr, total;
 };
 
 __host__ __device__ inline uint32_t lds_align4(uint32_t n) { return (n + 3u) & ~3u; }
 
-__host__ __device__ inline LdsLayout lds_layout(const Params& p, int slots) {
+__host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) {
   const uint32_t NE = (uint32_t)kEnvsPerBlock;
   const uint32_t streamW = (NE * (uint32_t)p.OB) >> 5;
   LdsLayout L;
@@ -94,12 +105,14 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int slots) {
   L.sB = o; o += lds_align4(streamW);
   L.spawnM = o; o += lds_align4(NE * (uint32_t)p.RW);
   L.wolfM = o; o += lds_align4(NE * (uint32_t)p.WHW);
+  L.bm = o; o += lds_align4(NE * (uint32_t)p.WHW);
+  L.masks = o; o += lds_align4(3u * (uint32_t)p.WHW);
   L.tiles = o; o += lds_align4((uint32_t)p.NT);
   L.snap = o; o += NE * 4u;
-  L.wl = o; o += lds_align4(NE * (uint32_t)slots);
   L.jobEnv = o; o += NE;
   L.jobKey = o; o += 2u * NE;
   L.blk = o; o += 4u;
+  L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
   L.total = o;
   return L;
 }

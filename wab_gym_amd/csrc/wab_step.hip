@@ -1,26 +1,28 @@
 // wab_step.hip — the fused batched Wolves-and-Bushes step for gfx950 (MI355X).
 //
 // One launch advances every env by one step (wab_env.py:250-342) and renders its
-// observation (wab_env.py:359-452); a second instantiation performs reset
+// observation (wab_env.py:359-452); the MODE_RESET instantiation performs reset
 // (wab_env.py:231-248).  One 256-thread workgroup owns 64 envs:
 //
-//   phase 0  all threads   zero the LDS bit-streams and masks, build the tile table
-//   phase 1  wave 0        lane = env: load SoA state, move, despawn, pursue, kill, eat,
-//                          hunger, starve; wolf + ostrich bits into stream A
-//   phase 2  all threads   tile-parallel keyed draws: bush presence for the W*H viewport
-//                          tiles -> stream A, wolf spawns on the margin ring -> spawn mask
-//   phase 3  wave 0        eaten-tile corrections, view mask, spawn -> slots, reward/done,
+//   phase A  all threads   zero the LDS bit-streams/masks, build the tile table
+//            wave 0        lane = env: issue every state load, apply the move, then scroll
+//                          the cached bush bitmap of the view by the move
+//   phase B  all threads   4 threads per env, keyed draws for the tiles that entered the
+//                          view (one row or column) -> bitmap, and for the wolf-spawn ring
+//                          around the new position -> spawn mask
+//   phase C  wave 0        eaten-tile corrections, bitmap -> bush plane, despawn, pursuit,
+//                          kill, eat, hunger, starve, spawn -> slots, reward/done, stores;
 //                          done-mask ballot -> compacted reset jobs (autoreset)
-//   phase 4  all threads   reset jobs: bush + initial-wolf draws for the new episode
-//                          -> stream B (skipped when the block has no done env)
-//   phase 5  wave 0        reset envs: wolves into slots, ostrich bit, view mask
-//   phase 6  all threads   expand the bit-streams 1 bit -> 1 byte and store the block's
+//   phase D  all threads   reset jobs: bush + initial-wolf draws over the new view
+//   phase E  wave 0        reset envs: bitmap -> plane, wolves -> slots, stores
+//   phase F  all threads   expand the bit-streams 1 bit -> 1 byte and store the block's
 //                          contiguous obs chunk with 16-byte coalesced stores
 //
 // The obs chunk of a block is 64 * 3*W*S contiguous bytes of `planes`; in LDS it is held
-// as a bit-stream whose bit k is byte k of the chunk, so every store of phase 6 is a full
-// 1 KiB wave-instruction regardless of W, H.  No MFMA: the work is integer hashing,
-// compares and byte stores.
+// as a bit-stream whose bit k is byte k of the chunk, so every store of phase F is a full
+// 1 KiB wave-instruction regardless of W, H.  Bush presence of the view is kept as a
+// W*H-bit bitmap per env in HBM (bushmap), so a step only hashes the <= max(W, H) tiles
+// that scroll into view instead of all W*H.  No MFMA: integer hashing, compares, bytes.
 #include <hip/hip_runtime.h>
 
 #include "wab_params.h"
@@ -29,6 +31,7 @@ namespace wab {
 
 enum : uint32_t { SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5 };
 enum { MODE_STEP = 0, MODE_RESET = 1 };
+enum { DIR_STAY = 0, DIR_RIGHT = 1, DIR_LEFT = 2, DIR_UP = 3, DIR_DOWN = 4 };
 
 // ------------------------------------------------------------------------ keyed RNG
 // Definition: oracle/keyed_rng.py (the golden vectors were generated under it).
@@ -60,12 +63,12 @@ __device__ __forceinline__ uint32_t draw_lo21(uint32_t h1, uint32_t ts, uint32_t
   return fmix32(h1 ^ rot ^ b0 ^ 0x9E3779B9u) >> 11;
 }
 
-// U >= thr for U = hi << 21 | lo21; the low half is only hashed when the high 32 bits tie
-// (probability 2^-32).  thr may be 2^53 ("never").
-__device__ __forceinline__ bool U_ge(uint32_t h1, uint32_t hi, uint32_t ts, uint32_t b0, uint64_t thr) {
-  const uint64_t th = thr >> 21;
-  if ((uint64_t)hi != th) return (uint64_t)hi > th;
-  return draw_lo21(h1, ts, b0) >= (uint32_t)(thr & 0x1FFFFFu);
+// U >= T for U = hi << 21 | lo21 and T = th << 21 | tl; the low half is only hashed when
+// the high 32 bits tie (probability 2^-32)
+__device__ __forceinline__ bool U_ge(uint32_t h1, uint32_t hi, uint32_t ts, uint32_t b0, uint32_t th,
+                                     uint32_t tl) {
+  if (hi != th) return hi > th;
+  return draw_lo21(h1, ts, b0) >= tl;
 }
 
 __device__ __forceinline__ uint64_t draw_U(uint32_t xy, uint32_t ts, uint32_t b0, uint32_t b1) {
@@ -74,14 +77,22 @@ __device__ __forceinline__ uint64_t draw_U(uint32_t xy, uint32_t ts, uint32_t b0
   return ((uint64_t)hi << 21) | draw_lo21(h1, ts, b0);
 }
 
-// number of thresholds T_k <= U: the reference's round(u**power * max) (wab_env.py:631-635)
-__device__ __forceinline__ int bush_value(const Params& p, uint64_t U) {
-  int lo = 0, hi = p.max_berries;
+// number of thresholds T_k <= U: the reference's round(u**power * max) (wab_env.py:631-635);
+// `thr` is the LDS copy of the table
+__device__ __forceinline__ int bush_value(const uint64_t* thr, int n, uint64_t U) {
+  int lo = 0, hi = n;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if (p.thresholds[mid] <= U) lo = mid + 1; else hi = mid;
+    if (thr[mid] <= U) lo = mid + 1; else hi = mid;
   }
   return lo;
+}
+
+// packed-tile add: both int16 halves wrap independently (v_pk_add_u16)
+typedef unsigned short wab_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t xy_add(uint32_t a, uint32_t b) {
+  wab_u16x2 va = __builtin_bit_cast(wab_u16x2, a), vb = __builtin_bit_cast(wab_u16x2, b);
+  return __builtin_bit_cast(uint32_t, va + vb);
 }
 
 __device__ __forceinline__ uint32_t udiv(uint32_t x, uint32_t d, uint32_t magic) {
@@ -92,7 +103,15 @@ __device__ __forceinline__ uint32_t udiv(uint32_t x, uint32_t d, uint32_t magic)
 }
 
 __device__ __forceinline__ void lds_set(uint32_t* s, uint32_t bit) { atomicOr(&s[bit >> 5], 1u << (bit & 31)); }
-__device__ __forceinline__ void lds_clear(uint32_t* s, uint32_t bit) { atomicAnd(&s[bit >> 5], ~(1u << (bit & 31))); }
+
+// OR the low `nbits` (<= 32) bits of v into the stream at bit offset `at`
+__device__ __forceinline__ void lds_or_bits(uint32_t* s, uint32_t at, uint32_t v, uint32_t nbits) {
+  if (nbits < 32) v &= (1u << nbits) - 1u;
+  if (!v) return;
+  const uint64_t m = (uint64_t)v << (at & 31);
+  atomicOr(&s[at >> 5], (uint32_t)m);
+  if (m >> 32) atomicOr(&s[(at >> 5) + 1], (uint32_t)(m >> 32));
+}
 
 // restrict_view: zero blind-spot cells of the three planes (mask_grid, wab_env.py:344-357)
 __device__ __forceinline__ void apply_view_mask(const Params& p, uint32_t* s, uint32_t env_bit, int role) {
@@ -108,36 +127,193 @@ __device__ __forceinline__ void apply_view_mask(const Params& p, uint32_t* s, ui
 
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
 
-// unpack a tile-table entry: world offset from the ostrich and bit index
+// Workgroup barrier for LDS hand-offs only.  Waves of a block exchange data exclusively
+// through LDS; __syncthreads() would also drain every outstanding global store
+// (s_waitcnt vmcnt(0)) and put HBM write latency on the critical path of each phase.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// tile-table entry: world offset from the ostrich (int8, int8) and a bit index
 __device__ __forceinline__ int tile_dx(uint32_t t) { return (int)(int8_t)(t & 0xFFu); }
 __device__ __forceinline__ int tile_dy(uint32_t t) { return (int)(int8_t)((t >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t tile_bit(uint32_t t) { return t >> 16; }
 
-template <int MODE, int SLOTS>
+// bitmap word k of env e: bm[k * NE + e] (slot-major: lanes of wave 0 hit consecutive banks)
+template <int NE>
+__device__ __forceinline__ uint32_t& BM(uint32_t* bm, int k, int e) { return bm[k * NE + e]; }
+
+// copy an env's W*H bush bitmap (bit i*H + j) into plane 1 of its stream segment
+template <int NE>
+__device__ __forceinline__ void bitmap_to_plane(const Params& p, uint32_t* bm, int e, uint32_t* s,
+                                                uint32_t at) {
+  if (p.S == p.H) {  // contiguous: one funnel-shifted copy
+    for (int k = 0; k < p.WHW; ++k) {
+      const uint32_t nb = min(32u, (uint32_t)(p.WH - 32 * k));
+      lds_or_bits(s, at + 32u * k, BM<NE>(bm, k, e), nb);
+    }
+  } else {           // padded rows: row i -> bits [i*S, i*S + H)
+    for (int i = 0; i < p.W; ++i) {
+      const uint32_t c = (uint32_t)(i * p.H);
+      for (int j0 = 0; j0 < p.H; j0 += 32) {
+        const uint32_t n = min(32u, (uint32_t)(p.H - j0));
+        const uint32_t b = c + j0;
+        uint64_t w = BM<NE>(bm, b >> 5, e) >> (b & 31);
+        if ((b & 31) + n > 32) w |= (uint64_t)BM<NE>(bm, (b >> 5) + 1, e) << (32 - (b & 31));
+        lds_or_bits(s, at + (uint32_t)(i * p.S + j0), (uint32_t)w, n);
+      }
+    }
+  }
+}
+
+// Diagnostic build (-DWAB_STAMPS): thread 0 of each block records s_memrealtime (100 MHz)
+// at phase boundaries into p.stamps; the product build compiles these to nothing.
+#ifdef WAB_STAMPS
+#define WAB_STAMP(slot)                                                                    \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && p.stamps)                                                      \
+      p.stamps[(size_t)blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+#else
+#define WAB_STAMP(slot) do {} while (0)
+#endif
+
+// 128-bit shifts of a W*H <= 128 bitmap held as two 64-bit halves
+__device__ __forceinline__ void shl128(uint64_t& lo, uint64_t& hi, int n) {
+  if (n >= 64) { hi = lo << (n - 64); lo = 0; }
+  else if (n > 0) { hi = (hi << n) | (lo >> (64 - n)); lo <<= n; }
+}
+__device__ __forceinline__ void shr128(uint64_t& lo, uint64_t& hi, int n) {
+  if (n >= 64) { lo = hi >> (n - 64); hi = 0; }
+  else if (n > 0) { lo = (lo >> n) | (hi << (64 - n)); hi >>= n; }
+}
+
+template <int MODE, int SLOTS, bool SMALL>
 __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr int NE = kEnvsPerBlock;
+  constexpr int G = kThreads / NE;  // threads per env in phase B
   const int tid = threadIdx.x;
   const int64_t g0 = (int64_t)blockIdx.x * NE;
   const int n_active = (int)min((int64_t)NE, p.B - g0);
   const uint32_t streamW = (uint32_t)(NE * p.OB) >> 5;
   const uint32_t plane = (uint32_t)(p.W * p.S);
+  const int NWd = SMALL ? min(p.WHW, 4) : p.WHW;
 
   const LdsLayout L = lds_layout(p, SLOTS);
   uint32_t* sA = lds + L.sA;          // step obs bits
   uint32_t* sB = lds + L.sB;          // reset obs bits
   uint32_t* spawnM = lds + L.spawnM;  // [NE][RW]
   uint32_t* wolfM = lds + L.wolfM;    // [job][WHW]
+  uint32_t* bm = lds + L.bm;          // [WHW][NE] bush bitmaps
+  uint32_t* masks = lds + L.masks;    // [3][WHW]: column 0, column H-1, valid bits
   uint32_t* tiles = lds + L.tiles;    // [NT]
-  uint32_t* snap = lds + L.snap;      // [NE][4]: pos, b0, b1, turn
-  uint32_t* wl = lds + L.wl;          // [SLOTS][NE] wolves (phase 1/3 scratch)
+  uint32_t* snap = lds + L.snap;      // [NE][4]: pos, b0, b1, turn20 | dir << 24
   uint32_t* jobEnv = lds + L.jobEnv;  // [NE]
   uint32_t* jobKey = lds + L.jobKey;  // [NE][2]
   uint32_t* blk = lds + L.blk;        // [0] n_jobs, [1..2] job mask
+  uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr);  // [max_berries] bush thresholds
 
-  // ---------------------------------------------------------------- phase 0
+  // per-env registers of wave 0 (lane = env)
+  const int e = tid;
+  const bool envlane = tid < NE;
+  const int64_t g = g0 + e;
+  const bool active = envlane && e < n_active;
+  int32_t ox = 0, oy = 0, turn = 0, role = 0, status = 0, nw = 0, ne = 0, ndep = 0, dir = DIR_STAY;
+  double food = 0.0, reward = 0.0;
+  uint32_t ep = 0, b0 = 0, b1 = 0;
+  bool done = false;
+  unsigned long long bad = 0, eaten_of = 0, wolf_of = 0;
+  // wolves of this env: slot registers + a live mask (slot order is irrelevant: co-located
+  // wolves are interchangeable, so only the multiset of positions is state)
+  uint32_t wr[SLOTS];
+  uint32_t live = 0;
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) wr[s] = 0u;
+
+  WAB_STAMP(0);
+  // ---------------------------------------------------------------- phase A
+  if (MODE == MODE_STEP && active) {
+    // every load is independent and issued up front: one memory round trip
+    const uint4 hdr = p.hdr[g];
+    const int a = (int)p.actions[g];
+    food = p.food[g];
+    const uint32_t w0 = p.wolves[g], w1 = p.wolves[p.B + g];  // slots 0, 1 speculatively
+    uint32_t bmr[4] = {0u, 0u, 0u, 0u};
+    if (SMALL) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < NWd) bmr[k] = p.bushmap[(int64_t)k * p.B + g];
+    } else {
+      for (int k = 0; k < NWd; ++k) BM<NE>(bm, k, e) = p.bushmap[(int64_t)k * p.B + g];
+    }
+    ox = xy_x(hdr.x);
+    oy = xy_y(hdr.x);
+    turn = (int32_t)hdr.y;
+    role = (int)misc_role(hdr.z);
+    status = (int)misc_status(hdr.z);
+    nw = (int)misc_nw(hdr.z);
+    ne = (int)misc_ne(hdr.z);
+    ndep = (int)misc_ndep(hdr.z);
+    ep = hdr.w;
+    wr[0] = w0;
+    wr[1] = w1;
+#pragma unroll
+    for (int s = 2; s < SLOTS; ++s)
+      if (s < nw) wr[s] = p.wolves[(int64_t)s * p.B + g];
+    live = nw >= 32 ? ~0u : ((1u << nw) - 1u);
+    turn += 1;                                                       // :252
+    if (a >= 0 && a < p.n_actions) {                                 // :253-258
+      const int dx = p.act_dx[a], dy = p.act_dy[a];
+      ox += dx;
+      oy += dy;
+      dir = dx > 0 ? DIR_RIGHT : dx < 0 ? DIR_LEFT : dy > 0 ? DIR_UP : dy < 0 ? DIR_DOWN : DIR_STAY;
+      if (p.act_role[a] >= 0) role = p.act_role[a];
+    } else {
+      bad += 1;
+    }
+    if (SMALL) {  // scroll the cached view bitmap by the move (:613-629 keeps old tiles)
+      uint64_t lo = (uint64_t)bmr[0] | ((uint64_t)bmr[1] << 32);
+      uint64_t hi = (uint64_t)bmr[2] | ((uint64_t)bmr[3] << 32);
+      if (dir == DIR_RIGHT || dir == DIR_UP) shl128(lo, hi, dir == DIR_RIGHT ? p.H : 1);
+      else if (dir == DIR_LEFT || dir == DIR_DOWN) shr128(lo, hi, dir == DIR_LEFT ? p.H : 1);
+      uint32_t v[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] &= p.small_masks[2][k];
+        if (dir == DIR_UP) v[k] &= ~p.small_masks[0][k];    // column 0 enters the view
+        if (dir == DIR_DOWN) v[k] &= ~p.small_masks[1][k];  // column H-1 enters the view
+        if (k < NWd) BM<NE>(bm, k, e) = v[k];
+      }
+    }
+    const uint64_t ek = episode_key(p.seed, (uint64_t)(p.env_base + g), ep);
+    b0 = (uint32_t)ek;
+    b1 = (uint32_t)(ek >> 32);
+    uint4 sn;
+    sn.x = xy_pack(ox, oy);
+    sn.y = b0;
+    sn.z = b1;
+    sn.w = ((uint32_t)turn & 0xFFFFFu) | ((uint32_t)dir << 24);
+    *reinterpret_cast<uint4*>(&snap[e * 4]) = sn;
+  }
   {
-    for (uint32_t i = tid; i < L.tiles; i += kThreads) lds[i] = 0;  // streams + masks
+    for (uint32_t i = tid; i < L.bm; i += kThreads) lds[i] = 0;  // streams + masks
+    if (!SMALL) {
+      for (int k = tid; k < NWd; k += kThreads) {                // column / validity masks
+        uint32_t c0 = 0, cl = 0, v = 0;
+        for (int b = 0; b < 32; ++b) {
+          const int c = 32 * k + b;
+          if (c >= p.WH) break;
+          v |= 1u << b;
+          const int j = c % p.H;
+          if (j == 0) c0 |= 1u << b;
+          if (j == p.H - 1) cl |= 1u << b;
+        }
+        masks[k] = c0;
+        masks[NWd + k] = cl;
+        masks[2 * NWd + k] = v;
+      }
+    }
     for (int c = tid; c < p.NT; c += kThreads) {
       int dx, dy;
       uint32_t bit;
@@ -158,164 +334,176 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
           yi = m + (r2 - band * p.H);
           xi = band < m ? band : band + p.W;
         }
-        dx = xi - p.cw - m;
-        dy = yi - p.ch - m;
-        bit = (uint32_t)r;
+        tiles[c] = xy_pack(xi - p.cw - m, yi - p.ch - m);  // ring: packed world offset
+        continue;
       }
       tiles[c] = ((uint32_t)dx & 0xFFu) | (((uint32_t)dy & 0xFFu) << 8) | (bit << 16);
     }
+    for (int k = tid; k < p.max_berries; k += kThreads) thr[k] = p.thresholds[k];
   }
-  __syncthreads();
-
-  // per-env registers of wave 0 (lane = env)
-  const int e = tid;
-  const bool envlane = tid < NE;
-  const int64_t g = g0 + e;
-  const bool active = envlane && e < n_active;
-  int32_t ox = 0, oy = 0, turn = 0, role = 0, status = 0, nw = 0, ne = 0;
-  double food = 0.0, reward = 0.0;
-  uint32_t ep = 0;
-  int eat_idx = -1;
-  bool done = false;
-  unsigned long long bad = 0, eaten_of = 0, wolf_of = 0;
+  lds_barrier();
 
   if constexpr (MODE == MODE_STEP) {
-    // -------------------------------------------------------------- phase 1 (wab_env.py:251-322)
-    if (active) {
-      const uint32_t pos = p.pos[g];
-      food = p.food[g];
-      turn = p.turn[g];
-      const uint32_t misc = p.misc[g];
-      ep = p.episode[g];
-      role = (int)(misc & 0xFFu);
-      status = (int)((misc >> 8) & 3u);
-      nw = (int)((misc >> 10) & 63u);
-      ne = (int)(misc >> 16);
-      ox = xy_x(pos);
-      oy = xy_y(pos);
-      const uint64_t ek = episode_key(p.seed, (uint64_t)(p.env_base + g), ep);
-      const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
-      const int a = (int)p.actions[g];
-      turn += 1;                                                   // :252
-      if (a >= 0 && a < p.n_actions) {                             // :253-258
-        ox += p.act_dx[a];
-        oy += p.act_dy[a];
-        if (p.act_role[a] >= 0) role = p.act_role[a];
-      } else {
-        bad += 1;
-      }
-      // despawn (:262-264): decide every wolf on the old list, then compact (stable)
-      for (int s = 0; s < nw; ++s) wl[s * NE + e] = p.wolves[(int64_t)s * p.B + g];
-      uint32_t keep = 0;
-      for (int s = 0; s < nw; ++s) {
-        const uint32_t w = wl[s * NE + e];
-        uint32_t k = 0;
-        for (int t = 0; t < s; ++t) k += (wl[t * NE + e] == w) ? 1u : 0u;
-        const uint32_t ts = make_ts(SITE_DESPAWN, k, turn);
-        const uint32_t h1 = fmix32(w ^ b0);
-        const uint32_t hi = fmix32(h1 ^ ts ^ b1);
-        if (U_ge(h1, hi, ts, b0, p.keep_gt + 1)) keep |= 1u << s;
-      }
-      int n = 0;
-      for (int s = 0; s < nw; ++s)
-        if (keep & (1u << s)) wl[(n++) * NE + e] = wl[s * NE + e];
-      nw = n;
-      // pursuit (:267-286): one axis step toward the ostrich, ties along x
-      if (p.wolves_can_move) {
-        for (int s = 0; s < nw; ++s) {
-          const uint32_t w = wl[s * NE + e];
-          int wx = xy_x(w), wy = xy_y(w);
-          const int ddx = ox - wx, ddy = oy - wy;
-          if (abs(ddx) >= abs(ddy)) wx += sgn(ddx); else wy += sgn(ddy);
-          wl[s * NE + e] = xy_pack(wx, wy);
+    WAB_STAMP(1);
+    if (!SMALL) {
+      // scroll the cached view bitmap by the move (generate_bushes keeps old tiles, :613-629)
+      if (active) {
+        if (dir == DIR_RIGHT || dir == DIR_UP) {        // shift toward higher bit indices
+          const int n = dir == DIR_RIGHT ? p.H : 1, q = n >> 5, r = n & 31;
+          for (int k = NWd - 1; k >= 0; --k) {
+            const uint32_t lo = k - q >= 0 ? BM<NE>(bm, k - q, e) : 0u;
+            const uint32_t lo2 = (r && k - q - 1 >= 0) ? BM<NE>(bm, k - q - 1, e) : 0u;
+            uint32_t v = r ? (lo << r) | (lo2 >> (32 - r)) : lo;
+            v &= masks[2 * NWd + k];
+            if (dir == DIR_UP) v &= ~masks[k];           // column 0 enters the view
+            BM<NE>(bm, k, e) = v;
+          }
+          // (RIGHT: row 0 = bits [0, H) arrive as zeros from the shift)
+        } else if (dir == DIR_LEFT || dir == DIR_DOWN) {  // shift toward lower bit indices
+          const int n = dir == DIR_LEFT ? p.H : 1, q = n >> 5, r = n & 31;
+          for (int k = 0; k < NWd; ++k) {
+            const uint32_t hi = k + q < NWd ? BM<NE>(bm, k + q, e) : 0u;
+            const uint32_t hi2 = (r && k + q + 1 < NWd) ? BM<NE>(bm, k + q + 1, e) : 0u;
+            uint32_t v = r ? (hi >> r) | (hi2 << (32 - r)) : hi;
+            v &= masks[2 * NWd + k];
+            if (dir == DIR_DOWN) v &= ~masks[NWd + k];   // column H-1 enters the view
+            BM<NE>(bm, k, e) = v;                         // (LEFT: row W-1 arrives as zeros)
+          }
         }
       }
-      // snapshot S (:289): wolves now, bushes with food > 0 now, status now
-      const int status_snap = status;
-      const uint32_t cpos = xy_pack(ox, oy);
+      lds_barrier();
+    }
+    WAB_STAMP(2);
+
+    // -------------------------------------------------------------- phase B (keyed draws)
+    {
+      const int be = tid / G, sub = tid - (tid / G) * G;
+      if (be < n_active) {
+        const uint4 sn = *reinterpret_cast<const uint4*>(&snap[be * 4]);
+        const uint32_t kb0 = sn.y;
+        // spawn ring around the new position (spawn_wolves :527-576): wolf iff u < p/2
+        const uint32_t ts_spawn = make_ts(SITE_SPAWN, 0, (int32_t)(sn.w & 0xFFFFFu));
+        const uint32_t hk = ts_spawn ^ sn.z;
+        uint32_t* sm = spawnM + be * p.RW;
+#pragma unroll 2
+        for (int r = sub; r < p.R; r += G) {
+          const uint32_t h1 = fmix32(xy_add(sn.x, tiles[p.WH + r]) ^ kb0);
+          const uint32_t hi = fmix32(h1 ^ hk);
+          if (hi <= p.spawn_th && (hi < p.spawn_th || draw_lo21(h1, ts_spawn, kb0) < p.spawn_tl))
+            atomicOr(&sm[r >> 5], 1u << (r & 31));
+        }
+        // the row or column that scrolled into view (generate_bushes :613-629)
+        const int bdir = (int)(sn.w >> 24);
+        if (bdir != DIR_STAY) {
+          const bool horiz = bdir == DIR_RIGHT || bdir == DIR_LEFT;
+          const int n = horiz ? p.H : p.W;
+          const int i0 = bdir == DIR_LEFT ? p.W - 1 : 0, j0 = bdir == DIR_DOWN ? p.H - 1 : 0;
+          const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), hb = ts_bush ^ sn.z;
+          const int bx = xy_x(sn.x), by = xy_y(sn.x);
+          for (int c = sub; c < n; c += G) {
+            const int i = horiz ? i0 : c, j = horiz ? c : j0;
+            const uint32_t h1 = fmix32(xy_pack(bx - (i - p.cw), by - (j - p.ch)) ^ kb0);
+            const uint32_t hi = fmix32(h1 ^ hb);
+            if (hi >= p.bush_th && (hi > p.bush_th || draw_lo21(h1, ts_bush, kb0) >= p.bush_tl)) {
+              const uint32_t cb = (uint32_t)(i * p.H + j);
+              atomicOr(&BM<NE>(bm, (int)(cb >> 5), be), 1u << (cb & 31));
+            }
+          }
+        }
+      }
+    }
+    lds_barrier();
+    WAB_STAMP(3);
+
+    // -------------------------------------------------------------- phase C (wab_env.py:259-342)
+    if (active) {
       const uint32_t ebit = (uint32_t)e * (uint32_t)p.OB;
-      for (int s = 0; s < nw; ++s) {  // wolf grid bits (:412-428)
-        const uint32_t w = wl[s * NE + e];
-        const int ddx = ox - xy_x(w), ddy = oy - xy_y(w);
-        if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) lds_set(sA, ebit + (uint32_t)((ddx + p.cw) * p.S + ddy + p.ch));
-        if (w == cpos && !p.god_mode) status = 2;                  // kill (:291-297)
+      const uint32_t cpos = xy_pack(ox, oy);
+      const uint32_t ccb = (uint32_t)(p.cw * p.H + p.ch);  // bitmap bit of the ostrich's tile
+      const bool center_bush = (BM<NE>(bm, ccb >> 5, e) >> (ccb & 31)) & 1u;
+      // eaten-tile log, read only when it can matter: for the berries left on the ostrich's
+      // tile, and for emptied tiles that may have scrolled back into view (absent from S, :506)
+      int found = -1;
+      if (center_bush || (ndep > 0 && dir != DIR_STAY)) {
+        for (int i = 0; i < ne; ++i) {
+          const uint32_t v = p.eaten_xy[(int64_t)i * p.B + g];
+          const int r = (int)p.eaten_rem[(int64_t)i * p.B + g];
+          if (v == cpos) found = i;
+          const int ddx = ox - xy_x(v), ddy = oy - xy_y(v);
+          if (r == 0 && abs(ddx) <= p.cw && abs(ddy) <= p.ch) {
+            const uint32_t cb = (uint32_t)((ddx + p.cw) * p.H + ddy + p.ch);
+            BM<NE>(bm, cb >> 5, e) &= ~(1u << (cb & 31));
+          }
+        }
+      }
+      WAB_STAMP(7);
+      bitmap_to_plane<NE>(p, bm, e, sA, ebit + plane);               // bush grid (:430-444)
+      WAB_STAMP(8);
+      // despawn (:262-264): one draw per wolf, keyed by its tile and its occurrence index
+      // among the co-located wolves before it
+      uint32_t keep = 0;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        if (!((live >> s) & 1u)) continue;
+        uint32_t k = 0;
+#pragma unroll
+        for (int t = 0; t < s; ++t) k += (((live >> t) & 1u) && wr[t] == wr[s]) ? 1u : 0u;
+        const uint32_t ts = make_ts(SITE_DESPAWN, k, turn);
+        const uint32_t h1 = fmix32(wr[s] ^ b0);
+        const uint32_t hi = fmix32(h1 ^ ts ^ b1);
+        if (U_ge(h1, hi, ts, b0, p.keep_th, p.keep_tl)) keep |= 1u << s;
+      }
+      live = keep;
+      // pursuit (:267-286): one axis step toward the ostrich, ties along x; then S (:289)
+      const int status_snap = status;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        if (!((live >> s) & 1u)) continue;
+        int wx = xy_x(wr[s]), wy = xy_y(wr[s]);
+        if (p.wolves_can_move) {
+          const int ddx = ox - wx, ddy = oy - wy;
+          if (abs(ddx) >= abs(ddy)) wx += sgn(ddx); else wy += sgn(ddy);
+          wr[s] = xy_pack(wx, wy);
+        }
+        const int ddx = ox - wx, ddy = oy - wy;
+        if (abs(ddx) <= p.cw && abs(ddy) <= p.ch)                     // wolf grid (:412-428)
+          lds_set(sA, ebit + (uint32_t)((ddx + p.cw) * p.S + ddy + p.ch));
+        if (ddx == 0 && ddy == 0 && !p.god_mode) status = 2;          // kill (:291-297)
       }
       lds_set(sA, ebit + 2 * plane + (uint32_t)(p.cw * p.S + p.ch));  // ostrich grid (:393-410)
+      WAB_STAMP(9);
       // berries left on the ostrich's tile: eaten log, else the tile's generated value
-      int found = -1;
-      for (int i = 0; i < ne; ++i) found = (p.eaten_xy[(int64_t)i * p.B + g] == cpos) ? i : found;
       int rem;
-      if (found >= 0) {
+      if (found >= 0)
         rem = p.eaten_rem[(int64_t)found * p.B + g];
-      } else {
-        const uint64_t U = draw_U(cpos, make_ts(SITE_BUSH, 0, 0), b0, b1);
-        rem = U >= p.bush_t1 ? bush_value(p, U) : 0;
-      }
+      else if (center_bush)
+        rem = bush_value(thr, p.max_berries, draw_U(cpos, make_ts(SITE_BUSH, 0, 0), b0, b1));
+      else
+        rem = 0;
       // eat (:299-313): stale snapshot status; clip only in this branch
       if (rem > 0 && status_snap == 0 && (role == 1 || p.lookout_only)) {
         food = food + p.fill;
         food = food < 0.0 ? 0.0 : (food > 1.0 ? 1.0 : food);
         reward += p.r_eat;
+        bool logged = true;
         if (found >= 0) {
           p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
-          eat_idx = found;
         } else if (ne < p.eaten_cap) {
           p.eaten_xy[(int64_t)ne * p.B + g] = cpos;
           p.eaten_rem[(int64_t)ne * p.B + g] = (uint8_t)(rem - 1);
-          eat_idx = ne;
           ne += 1;
         } else {
           eaten_of += 1;
+          logged = false;
+        }
+        if (rem == 1) {  // emptied: gone from the cached view from the next step on
+          BM<NE>(bm, ccb >> 5, e) &= ~(1u << (ccb & 31));
+          if (logged) ndep += 1;
         }
       }
-      food = food - p.hunger;                                      // :316
-      if (food <= 0.0) { status = 1; food = 0.0; }                 // :319-322
-      uint4 sn;
-      sn.x = cpos; sn.y = b0; sn.z = b1; sn.w = (uint32_t)turn;
-      *reinterpret_cast<uint4*>(&snap[e * 4]) = sn;
-    }
-    __syncthreads();
-
-    // -------------------------------------------------------------- phase 2 (tile-parallel draws)
-    {
-      const int NT = p.NT;
-      const int items = n_active * NT;
-      int ie = tid / NT, ic = tid - (tid / NT) * NT;
-      const int stepE = kThreads / NT, stepC = kThreads - (kThreads / NT) * NT;
-      const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
-      for (int q = tid; q < items; q += kThreads) {
-        const uint4 sn = *reinterpret_cast<const uint4*>(&snap[ie * 4]);
-        const uint32_t t = tiles[ic];
-        const uint32_t xy = xy_pack(xy_x(sn.x) + tile_dx(t), xy_y(sn.x) + tile_dy(t));
-        const bool is_bush = ic < p.WH;
-        const uint32_t ts = is_bush ? ts_bush : make_ts(SITE_SPAWN, 0, (int32_t)sn.w);
-        const uint64_t thr = is_bush ? p.bush_t1 : p.spawn_lt;
-        const uint32_t h1 = fmix32(xy ^ sn.y);
-        const uint32_t hi = fmix32(h1 ^ ts ^ sn.z);
-        const bool ge = U_ge(h1, hi, ts, sn.y, thr);
-        if (is_bush) {
-          if (ge) lds_set(sA, (uint32_t)ie * (uint32_t)p.OB + plane + tile_bit(t));   // bush present
-        } else if (!ge) {
-          lds_set(spawnM + ie * p.RW, tile_bit(t));                                  // wolf spawns
-        }
-        ic += stepC;
-        ie += stepE;
-        if (ic >= NT) { ic -= NT; ie += 1; }
-      }
-    }
-    __syncthreads();
-
-    // -------------------------------------------------------------- phase 3
-    if (active) {
-      const uint32_t ebit = (uint32_t)e * (uint32_t)p.OB;
-      // bushes emptied before this step's eat are absent from S (:506): clear them
-      for (int i = 0; i < ne; ++i) {
-        const uint32_t v = p.eaten_xy[(int64_t)i * p.B + g];
-        const int r = (int)p.eaten_rem[(int64_t)i * p.B + g] + (i == eat_idx ? 1 : 0);
-        const int ddx = ox - xy_x(v), ddy = oy - xy_y(v);
-        if (r == 0 && abs(ddx) <= p.cw && abs(ddy) <= p.ch)
-          lds_clear(sA, ebit + plane + (uint32_t)((ddx + p.cw) * p.S + ddy + p.ch));
-      }
+      WAB_STAMP(10);
+      food = food - p.hunger;                                        // :316
+      if (food <= 0.0) { status = 1; food = 0.0; }                   // :319-322
       if (p.restrict_view) apply_view_mask(p, sA, ebit, role);
       // spawn_wolves (:325-326, :527-576) on the ring around the new position
       for (int wd = 0; wd < p.RW; ++wd) {
@@ -323,11 +511,15 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
         while (bits) {
           const int b = __ffs(bits) - 1;
           bits &= bits - 1;
-          const uint32_t t = tiles[p.WH + wd * 32 + b];
-          if (nw < SLOTS) wl[(nw++) * NE + e] = xy_pack(ox + tile_dx(t), oy + tile_dy(t));
-          else wolf_of += 1;
+          const uint32_t w = xy_add(cpos, tiles[p.WH + wd * 32 + b]);
+          bool placed = false;
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s)
+            if (!placed && !((live >> s) & 1u)) { wr[s] = w; live |= 1u << s; placed = true; }
+          if (!placed) wolf_of += 1;
         }
       }
+      WAB_STAMP(11);
       // reward / done (:328-340)
       if (status == 0) {
         if (turn >= p.max_turns) { reward += p.r_finish; done = true; }
@@ -342,9 +534,13 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
     }
   } else {
     // reset mode: the flagged envs become reset jobs
-    if (active) done = (p.reset_mask == nullptr) || (p.reset_mask[g] != 0);
+    if (active) {
+      done = (p.reset_mask == nullptr) || (p.reset_mask[g] != 0);
+      if (done) ep = p.hdr[g].w;
+    }
   }
 
+  WAB_STAMP(12);
   // ---------------------------------------------------------------- done-mask ballot -> jobs
   const bool job = active && done && (MODE == MODE_RESET || p.autoreset);
   unsigned long long jm = 0;
@@ -357,26 +553,28 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
     }
   }
   if (active) {
-    const int ft = (int)ceil(food * (double)p.turns_empty);       // :450-452
     if (job) {
       if (MODE == MODE_STEP && p.t_planes) {
-        p.t_food_turns[g] = (uint8_t)ft;
+        p.t_food_turns[g] = (uint8_t)(int)ceil(food * (double)p.turns_empty);
         p.t_role[g] = (uint8_t)role;
         p.t_status[g] = (uint8_t)status;
       }
       // reset (:231-248, spawn_ostriches :595-611)
       const int j = __popcll(jm & ((1ull << e) - 1ull));
-      ep = (MODE == MODE_RESET) ? p.episode[g] + 1u : ep + 1u;
+      ep += 1u;  // 0xFFFFFFFF -> 0 on the first reset
       const uint64_t ek = episode_key(p.seed, (uint64_t)(p.env_base + g), ep);
-      const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+      b0 = (uint32_t)ek;
+      b1 = (uint32_t)(ek >> 32);
       jobEnv[j] = (uint32_t)e;
       jobKey[2 * j] = b0;
       jobKey[2 * j + 1] = b1;
+      for (int k = 0; k < NWd; ++k) BM<NE>(bm, k, e) = 0u;
       turn = 0;
       ox = 0;
       oy = 0;
       status = 0;
       ne = 0;
+      ndep = 0;
       nw = 0;
       food = p.start_food_random
                  ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), b0, b1) * 0x1p-53
@@ -384,19 +582,23 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       role = p.start_role_random
                  ? (int)(draw_U(xy_pack(0, 0), make_ts(SITE_START_ROLE, 0, 0), b0, b1) >> 52)
                  : p.start_role;
-      p.episode[g] = ep;
     }
     if (MODE == MODE_STEP || job) {
-      p.food_turns[g] = (uint8_t)(int)ceil(food * (double)p.turns_empty);
+      p.food_turns[g] = (uint8_t)(int)ceil(food * (double)p.turns_empty);  // :450-452
       p.role[g] = (uint8_t)role;
       p.status[g] = (uint8_t)status;
-      p.pos[g] = xy_pack(ox, oy);
       p.food[g] = food;
-      p.turn[g] = turn;
     }
     if (MODE == MODE_STEP && !job) {
-      for (int s = 0; s < nw; ++s) p.wolves[(int64_t)s * p.B + g] = wl[s * NE + e];
-      p.misc[g] = misc_pack((uint32_t)role, (uint32_t)status, (uint32_t)nw, (uint32_t)ne);
+      nw = 0;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s)
+        if ((live >> s) & 1u) p.wolves[(int64_t)(nw++) * p.B + g] = wr[s];
+      for (int k = 0; k < NWd; ++k) p.bushmap[(int64_t)k * p.B + g] = BM<NE>(bm, k, e);
+      p.hdr[g] = make_uint4(xy_pack(ox, oy), (uint32_t)turn,
+                            misc_pack((uint32_t)role, (uint32_t)status, (uint32_t)nw, (uint32_t)ne,
+                                      (uint32_t)ndep),
+                            ep);
     }
   }
   if (envlane && (bad | eaten_of | wolf_of)) {
@@ -404,12 +606,13 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
     if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
     if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
   }
-  __syncthreads();
+  lds_barrier();
+  WAB_STAMP(4);
 
   const int n_jobs = (int)blk[0];
   const unsigned long long done_mask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
   if (n_jobs > 0) {
-    // -------------------------------------------------------------- phase 4 (reset draws)
+    // -------------------------------------------------------------- phase D (reset draws)
     {
       const int WH = p.WH;
       const int items = n_jobs * WH;
@@ -417,17 +620,17 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       const int stepJ = kThreads / WH, stepC = kThreads - (kThreads / WH) * WH;
       const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), ts_wolf = make_ts(SITE_SPAWN, 0, 0);
       for (int q = tid; q < items; q += kThreads) {
-        const uint32_t je = jobEnv[ij], b0 = jobKey[2 * ij], b1 = jobKey[2 * ij + 1];
+        const uint32_t je = jobEnv[ij], kb0 = jobKey[2 * ij], kb1 = jobKey[2 * ij + 1];
         const uint32_t t = tiles[ic];
         const uint32_t xy = xy_pack(tile_dx(t), tile_dy(t));  // ostrich at (0, 0)
-        const uint32_t h1 = fmix32(xy ^ b0);
-        const uint32_t ebit = je * (uint32_t)p.OB;
-        const uint32_t hb = fmix32(h1 ^ ts_bush ^ b1);
-        if (U_ge(h1, hb, ts_bush, b0, p.bush_t1)) lds_set(sB, ebit + plane + tile_bit(t));   // generate_bushes
-        if (p.wolves_on) {                                                                  // initialize_wolves
-          const uint32_t hw = fmix32(h1 ^ ts_wolf ^ b1);
-          if (!U_ge(h1, hw, ts_wolf, b0, p.spawn_lt)) {
-            lds_set(sB, ebit + tile_bit(t));
+        const uint32_t h1 = fmix32(xy ^ kb0);
+        const uint32_t hb = fmix32(h1 ^ ts_bush ^ kb1);
+        if (U_ge(h1, hb, ts_bush, kb0, p.bush_th, p.bush_tl))         // generate_bushes
+          atomicOr(&BM<NE>(bm, ic >> 5, (int)je), 1u << (ic & 31));
+        if (p.wolves_on) {                                               // initialize_wolves
+          const uint32_t hw = fmix32(h1 ^ ts_wolf ^ kb1);
+          if (!U_ge(h1, hw, ts_wolf, kb0, p.spawn_th, p.spawn_tl)) {
+            lds_set(sB, je * (uint32_t)p.OB + tile_bit(t));
             lds_set(wolfM + ij * p.WHW, (uint32_t)ic);
           }
         }
@@ -436,11 +639,13 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
         if (ic >= WH) { ic -= WH; ij += 1; }
       }
     }
-    __syncthreads();
-    // -------------------------------------------------------------- phase 5 (reset envs)
+    lds_barrier();
+    // -------------------------------------------------------------- phase E (reset envs)
     if (job) {
       const int j = __popcll(done_mask & ((1ull << e) - 1ull));
       const uint32_t ebit = (uint32_t)e * (uint32_t)p.OB;
+      bitmap_to_plane<NE>(p, bm, e, sB, ebit + plane);
+      for (int k = 0; k < NWd; ++k) p.bushmap[(int64_t)k * p.B + g] = BM<NE>(bm, k, e);
       lds_set(sB, ebit + 2 * plane + (uint32_t)(p.cw * p.S + p.ch));
       if (p.restrict_view) apply_view_mask(p, sB, ebit, role);
       int n = 0;
@@ -454,13 +659,14 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
           else atomicAdd(&p.counters[0], 1ull);
         }
       }
-      p.misc[g] = misc_pack((uint32_t)role, 0u, (uint32_t)n, 0u);
+      p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role, 0u, (uint32_t)n, 0u, 0u), ep);
     }
     if (tid == 0) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
-    __syncthreads();
+    lds_barrier();
   }
+  WAB_STAMP(5);
 
-  // ---------------------------------------------------------------- phase 6 (expand + store)
+  // ---------------------------------------------------------------- phase F (expand + store)
   {
     const uint32_t OB = (uint32_t)p.OB;
     const uint32_t limit = (uint32_t)n_active * OB;      // valid bytes of this block's chunk
@@ -468,19 +674,19 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
     uint8_t* tout = (MODE == MODE_STEP && p.t_planes) ? p.t_planes + (size_t)g0 * OB : nullptr;
     const bool full_jobs = (MODE == MODE_RESET) && n_jobs == n_active;
     for (uint32_t d = tid; d < streamW; d += kThreads) {
-      const uint32_t b0 = d << 5;
-      if (b0 >= limit) break;
+      const uint32_t bo = d << 5;
+      if (bo >= limit) break;
       uint32_t dm = 0;   // bits of this dword that belong to job (done / flagged) envs
       if (n_jobs > 0) {
         if (full_jobs) {
           dm = ~0u;
         } else {
-          const uint32_t e_lo = udiv(b0, OB, p.magic_OB);
-          const uint32_t e_hi = min(udiv(b0 + 31u, OB, p.magic_OB), (uint32_t)NE - 1u);
+          const uint32_t e_lo = udiv(bo, OB, p.magic_OB);
+          const uint32_t e_hi = min(udiv(bo + 31u, OB, p.magic_OB), (uint32_t)NE - 1u);
           for (uint32_t ee = e_lo; ee <= e_hi; ++ee) {
             if (!((done_mask >> ee) & 1ull)) continue;
-            const uint32_t lo = max(ee * OB, b0) - b0;
-            const uint32_t hi = min((ee + 1u) * OB, b0 + 32u) - b0;  // exclusive, <= 32
+            const uint32_t lo = max(ee * OB, bo) - bo;
+            const uint32_t hi = min((ee + 1u) * OB, bo + 32u) - bo;  // exclusive, <= 32
             dm |= (hi >= 32u ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
           }
         }
@@ -489,29 +695,32 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       if (MODE == MODE_STEP) v = (sA[d] & ~dm) | (sB[d] & dm);
       else v = sB[d];
       const uint32_t write_mask = (MODE == MODE_STEP) ? ~0u : dm;
-      if (write_mask == ~0u && b0 + 32u <= limit) {
+      if (write_mask == ~0u && bo + 32u <= limit) {
         uint4 q0, q1;
 #pragma unroll
         for (int k = 0; k < 4; ++k) (&q0.x)[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) (&q1.x)[k] = (((v >> (16 + 4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-        *reinterpret_cast<uint4*>(out + b0) = q0;
-        *reinterpret_cast<uint4*>(out + b0 + 16) = q1;
+        *reinterpret_cast<uint4*>(out + bo) = q0;
+        *reinterpret_cast<uint4*>(out + bo + 16) = q1;
       } else if (write_mask) {
-        for (uint32_t k = 0; k < 32u && b0 + k < limit; ++k)
-          if ((write_mask >> k) & 1u) out[b0 + k] = (uint8_t)((v >> k) & 1u);
+        for (uint32_t k = 0; k < 32u && bo + k < limit; ++k)
+          if ((write_mask >> k) & 1u) out[bo + k] = (uint8_t)((v >> k) & 1u);
       }
       if (MODE == MODE_STEP && tout && dm) {
         const uint32_t va = sA[d];
-        for (uint32_t k = 0; k < 32u && b0 + k < limit; ++k)
-          if ((dm >> k) & 1u) tout[b0 + k] = (uint8_t)((va >> k) & 1u);
+        for (uint32_t k = 0; k < 32u && bo + k < limit; ++k)
+          if ((dm >> k) & 1u) tout[bo + k] = (uint8_t)((va >> k) & 1u);
       }
     }
   }
+  WAB_STAMP(6);
 }
 
 // explicit instantiations used by wab_capi.hip
-#define WAB_INST(M, S) template __global__ void wab_kernel<M, S>(Params);
+#define WAB_INST(M, S)                                           \
+  template __global__ void wab_kernel<M, S, true>(Params);       \
+  template __global__ void wab_kernel<M, S, false>(Params);
 WAB_INST(MODE_STEP, 8)
 WAB_INST(MODE_STEP, 16)
 WAB_INST(MODE_STEP, 32)
