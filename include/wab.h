@@ -21,6 +21,9 @@
  *   wab_rollout           <- the per-step loop of actor_critic.main  actor_critic.py:185-200
  *                            with pre-chosen actions (T fused steps)
  *   wab_destroy           <- (gym.Env.close; nothing to free in the reference)
+ *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
+ *                            + gym.spaces.flatten                    actor_critic.py:188
+ *   wab_discounted_returns<- finish_episode's return loop             actor_critic.py:139-143
  */
 #ifndef WAB_H_
 #define WAB_H_
@@ -163,8 +166,28 @@ int wab_get_counters(wab_handle* h, wab_counters* out, void* stream);
 int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* turn,
                   int32_t* n_wolves, uint32_t* episode, void* stream);
 
-/* Batch size and global-id base of a handle. */
+/* Batch size of a handle. */
 int64_t wab_batch(const wab_handle* h);
+
+/* ---- config 5 (actor_critic.py rollout) ------------------------------------------ */
+
+/* Length of the flattened PragmaticObsWrapper observation for the handle's options
+ * (449 for the defaults), or WAB_E_INVALID if the wrapper cannot index the grids. */
+int wab_feature_dim(const wab_handle* h);
+
+/* PragmaticObsWrapper.observation (wab_env.py:726-824) + gym 0.17 spaces.flatten
+ * (actor_critic.py:188) on device: obs -> features [B][F] float32 one-hot values.
+ * view_mask: [B][11][11] u8 device pointer, or NULL to derive it from role and the
+ * options as _get_obs does (wab_env.py:360-368). */
+int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
+                  void* stream);
+
+/* Discounted returns of actor_critic.finish_episode (actor_critic.py:139-143) over a
+ * [T][B] rollout: R_t = r_t + gamma * R_{t+1}, restarted after every done_t, R_T =
+ * bootstrap[b] (NULL = 0).  Accumulated in double as the reference's Python floats are;
+ * written as f32.  All pointers device. */
+int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, int64_t B,
+                           double gamma, const float* bootstrap, float* returns, void* stream);
 
 #ifdef __cplusplus
 }

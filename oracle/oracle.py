@@ -48,6 +48,9 @@ def lib():
         L.wabo_draw_U.restype = ctypes.c_uint64
         L.wabo_draw_U.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_uint32]
+        L.wabo_feature_dim.argtypes = [ctypes.c_int] * 3
+        L.wabo_featurize.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 6
+        L.wabo_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_double, P, P]
         _lib = L
     return _lib
 
@@ -119,3 +122,29 @@ def episode_key(seed, env, episode):
 
 def draw_U(ek, site, turn, x, y, k=0):
     return int(lib().wabo_draw_U(ek, site, turn, x, y, k))
+
+
+def feature_dim(W, H, turns_empty=40):
+    return int(lib().wabo_feature_dim(W, H, turns_empty))
+
+
+def featurize(planes, food_turns, role, status, view_mask, W, H, turns_empty=40):
+    """planes [B,3,W,S] u8, scalars [B] u8, view_mask [B,11,11] u8 -> float32 [B, F]."""
+    planes = np.ascontiguousarray(planes, dtype=np.uint8)
+    B, S = planes.shape[0], planes.shape[3]
+    F = feature_dim(W, H, turns_empty)
+    out = np.zeros((B, F), np.float32)
+    arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in (food_turns, role, status, view_mask)]
+    lib().wabo_featurize(B, W, H, S, turns_empty, _p(planes), _p(arrs[0]), _p(arrs[1]), _p(arrs[2]),
+                         _p(arrs[3]), _p(out))
+    return out
+
+
+def discounted_returns(reward, done, gamma=0.99, bootstrap=None):
+    reward = np.ascontiguousarray(reward, dtype=np.float32)
+    done = np.ascontiguousarray(done, dtype=np.uint8)
+    T, B = reward.shape
+    out = np.zeros((T, B), np.float32)
+    bs = None if bootstrap is None else np.ascontiguousarray(bootstrap, dtype=np.float32)
+    lib().wabo_discounted_returns(T, B, _p(reward), _p(done), gamma, _p(bs), _p(out))
+    return out

@@ -367,3 +367,95 @@ void wabo_get_state(const wabo_batch* b, double* food, int32_t* x, int32_t* y, i
     if (episode) episode[i] = (uint32_t)e->episode;
   }
 }
+
+/* ------------------------------------------------------------------ config-5 featurizer */
+/* PragmaticObsWrapper.observation (wab_env.py:726-824) followed by gym 0.17 spaces.flatten
+ * (actor_critic.py:188): Discrete(n) -> one-hot(n) float32, Tuple -> concatenation,
+ * Box -> ravel.  planes [B][3][W][S] u8; view_mask [B][11][11] u8; out [B][F] f32. */
+int wabo_feature_dim(int W, int H, int turns_empty) {
+  const int md = W / 2 + H / 2 + 1;
+  return 16 * (md + 1) + 88 + 2 + (turns_empty + 1) + 2 + 3 + 121;
+}
+
+static void nearest_things(const uint8_t* g, int W, int H, int S, int md, int near[4], int second[4],
+                           int counts[4]) {
+  int shortest = md, second_d = md;
+  int si[2] = {0, 0}, s2[2] = {0, 0};
+  int any = 0;
+  counts[0] = counts[1] = counts[2] = counts[3] = 0;
+  for (int r = 0; r < W; ++r)          /* np.where: row-major over (axis 0, axis 1) :770 */
+    for (int c = 0; c < H; ++c) {
+      if (g[r * S + c] != 1) continue;
+      any = 1;
+      const int rr = r - H / 2, rc = c - W / 2;   /* :779-780 (axis 0 measured with H) */
+      const int tx = abs(rr) + abs(rc);
+      if (tx <= shortest) {                        /* :782-787 */
+        second_d = shortest;
+        s2[0] = si[0]; s2[1] = si[1];
+        shortest = tx;
+        si[0] = rr; si[1] = rc;
+      } else if (tx <= second_d) {                 /* :788-791 */
+        second_d = tx;
+        s2[0] = rr; s2[1] = rc;
+      }
+      if (r < H / 2) counts[0]++;                  /* up    binary_map[0:half_row, :]   :819 */
+      if (c > W / 2) counts[1]++;                  /* right binary_map[:, half_col+1:]  :820 */
+      if (r > H / 2) counts[2]++;                  /* down  binary_map[half_row+1:, :]  :821 */
+      if (c < W / 2) counts[3]++;                  /* left  binary_map[:, 0:half_col]   :822 */
+    }
+  for (int k = 0; k < 4; ++k) counts[k] = counts[k] < 10 ? counts[k] : 10;  /* :734, :737 */
+  if (!any) {
+    for (int k = 0; k < 4; ++k) near[k] = second[k] = 0;
+    return;
+  }
+  const int* idx[2] = {si, s2};
+  int* outp[2] = {near, second};
+  for (int q = 0; q < 2; ++q) {                    /* :792-808 */
+    const int a = idx[q][0], b = idx[q][1];
+    const int up = a < 0 ? -a : 0, right = b > 0 ? b : 0, down = a > 0 ? a : 0, left = b < 0 ? -b : 0;
+    outp[q][0] = up ? md - up : 0;
+    outp[q][1] = right ? md - right : 0;
+    outp[q][2] = down ? md - down : 0;
+    outp[q][3] = left ? md - left : 0;
+  }
+}
+
+void wabo_featurize(int64_t B, int W, int H, int S, int turns_empty, const uint8_t* planes,
+                    const uint8_t* food_turns, const uint8_t* role, const uint8_t* status,
+                    const uint8_t* view_mask, float* out) {
+  const int md = W / 2 + H / 2 + 1;
+  const int F = wabo_feature_dim(W, H, turns_empty);
+  for (int64_t i = 0; i < B; ++i) {
+    const uint8_t* pl = planes + (size_t)i * 3 * W * S;
+    float* o = out + (size_t)i * F;
+    memset(o, 0, sizeof(float) * (size_t)F);
+    int nw[4], sw[4], cw[4], nb[4], sb[4], cb[4];
+    nearest_things(pl, W, H, S, md, nw, sw, cw);
+    nearest_things(pl + W * S, W, H, S, md, nb, sb, cb);
+    int off = 0;
+    const int* groups[6] = {nw, sw, cw, nb, sb, cb};
+    const int sizes[6] = {md + 1, md + 1, 11, md + 1, md + 1, 11};
+    for (int gq = 0; gq < 6; ++gq)
+      for (int k = 0; k < 4; ++k) { o[off + groups[gq][k]] = 1.0f; off += sizes[gq]; }
+    const int standing = pl[W * S + (md / 2) * S + md / 2];  /* bushes[md//2, md//2] :742 */
+    o[off + standing] = 1.0f; off += 2;
+    o[off + food_turns[i]] = 1.0f; off += turns_empty + 1;
+    o[off + role[i]] = 1.0f; off += 2;
+    o[off + status[i]] = 1.0f; off += 3;
+    for (int k = 0; k < 121; ++k) o[off + k] = (float)view_mask[(size_t)i * 121 + k];
+  }
+}
+
+/* actor_critic.finish_episode returns (actor_critic.py:139-143): per env, reverse
+ * R = r + gamma * R in double (Python floats), restarting after each done; f32 out */
+void wabo_discounted_returns(int64_t T, int64_t B, const float* reward, const uint8_t* done,
+                             double gamma, const float* bootstrap, float* out) {
+  for (int64_t b = 0; b < B; ++b) {
+    double R = bootstrap ? (double)bootstrap[b] : 0.0;
+    for (int64_t t = T - 1; t >= 0; --t) {
+      if (done[t * B + b]) R = 0.0;
+      R = (double)reward[t * B + b] + gamma * R;
+      out[t * B + b] = (float)R;
+    }
+  }
+}

@@ -1,0 +1,72 @@
+"""Config 5 on CPU: the oracle's PragmaticObsWrapper restatement matches the reference's own
+KATs (wab_env_test.py) and the reference-generated golden vectors; returns follow
+actor_critic.finish_episode."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pragmatic.npz")
+MD = 11
+
+
+def _decode(f):
+    """float features [449] -> the wrapper's 11-tuple (one-hot groups back to values)."""
+    off, groups = 0, []
+    for n, size in [(4, MD + 1), (4, MD + 1), (4, 11), (4, MD + 1), (4, MD + 1), (4, 11)]:
+        g = []
+        for _ in range(n):
+            g.append(int(np.argmax(f[off:off + size])))
+            off += size
+        groups.append(g)
+    standing = int(np.argmax(f[off:off + 2]))
+    return groups, standing, None
+
+
+def test_reference_kats():
+    """The three known-answer tests of the reference (wab_env_test.py:9-169)."""
+    z = np.load(GOLDEN)
+    feats = orc.featurize(z["planes"][:3], z["scalars"][:3, 0], z["scalars"][:3, 1],
+                          z["scalars"][:3, 2], z["view_mask"][:3], 11, 11)
+    g0, _, _ = _decode(feats[0])
+    assert g0[0] == [0, 0, 0, 0] and g0[1] == [0, 10, 10, 0] and g0[2] == [1, 1, 1, 1]
+    assert g0[3] == [0, 0, 9, 10] and g0[4] == [0, 0, 10, 9] and g0[5] == [0, 2, 4, 2]
+    _, standing, _ = _decode(feats[1])
+    assert standing == 1
+    g2, _, _ = _decode(feats[2])
+    assert g2[0] == [0, 10, 0, 0] and g2[1] == [0, 10, 10, 0] and g2[2] == [10, 10, 5, 4]
+    assert g2[3] == [0, 0, 7, 0] and g2[4] == [7, 0, 0, 0] and g2[5] == [7, 6, 7, 6]
+
+
+def test_oracle_featurizer_matches_reference_golden():
+    z = np.load(GOLDEN)
+    feats = orc.featurize(z["planes"], z["scalars"][:, 0], z["scalars"][:, 1], z["scalars"][:, 2],
+                          z["view_mask"], 11, 11)
+    assert feats.shape[1] == int(z["flatdim"]) == 449
+    assert np.array_equal(feats, z["features"])
+
+
+def _returns_reference(rewards, gamma=0.99):
+    R, out = 0, []
+    for r in rewards[::-1]:          # actor_critic.py:139-143
+        R = r + gamma * R
+        out.insert(0, R)
+    return out
+
+
+def test_discounted_returns_match_finish_episode():
+    rng = np.random.RandomState(0)
+    T, B = 90, 37
+    reward = rng.choice([0.0, 0.1, -1.0, 1.0, -0.9, 1.1], size=(T, B)).astype(np.float32)
+    done = (rng.random_sample((T, B)) < 0.05).astype(np.uint8)
+    done[-1] = 1
+    got = orc.discounted_returns(reward, done)
+    for b in range(B):
+        start = 0
+        for t in range(T):
+            if done[t, b]:
+                want = np.float32(_returns_reference([float(x) for x in reward[start:t + 1, b]]))
+                assert np.array_equal(got[start:t + 1, b], want)
+                start = t + 1

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("WAB_LIB") or os.path.join(HERE, "_lib", "libwab_hip.s
 EXPORTED = [
     "wab_abi_version", "wab_last_error", "wab_num_actions", "wab_create", "wab_destroy",
     "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
+    "wab_feature_dim", "wab_featurize", "wab_discounted_returns",
 ]
 
 ABI_VERSION = 1
@@ -62,6 +63,9 @@ def load():
     L.wab_rollout.argtypes = [P, P, I32, P, P, P, P]
     L.wab_get_counters.argtypes = [P, P, P]
     L.wab_get_state.argtypes = [P, P, P, P, P, P, P, P]
+    L.wab_feature_dim.argtypes = [P]
+    L.wab_featurize.argtypes = [P, P, P, P, P]
+    L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64
     for name in EXPORTED:

@@ -17,6 +17,21 @@
 namespace wab {
 template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
+
+struct FeatParams {
+  int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
+  int64_t B;
+  uint32_t mask_rows[2][11];
+  const uint8_t* planes;
+  const uint8_t* food_turns;
+  const uint8_t* role;
+  const uint8_t* status;
+  const uint8_t* view_mask;
+  float* out;
+};
+__global__ void wab_featurize_kernel(FeatParams p);
+__global__ void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T, int64_t B,
+                                   double gamma, const float* bootstrap, float* out);
 }
 
 using wab::Params;
@@ -409,6 +424,63 @@ int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* 
     if (n_wolves) n_wolves[i] = (int32_t)wab::misc_nw(hdr[i].z);
     if (episode) episode[i] = hdr[i].w;
   }
+  return WAB_OK;
+}
+
+int wab_feature_dim(const wab_handle* h) {
+  if (!h) return WAB_E_INVALID;
+  const Params& p = h->p;
+  const int md = p.W / 2 + p.H / 2 + 1;
+  if (md / 2 >= p.W || md / 2 >= p.H) return WAB_E_INVALID;  // bushes[md//2, md//2] (wab_env.py:742)
+  return 16 * (md + 1) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121;
+}
+
+int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
+                  void* stream) {
+  g_err.clear();
+  if (!h || !features) return fail(WAB_E_INVALID, "wab_featurize: NULL argument");
+  if (int rc = check_obs(obs, "wab_featurize")) return rc;
+  const int F = wab_feature_dim(h);
+  if (F < 0) return fail(WAB_E_INVALID, "wab_featurize: PragmaticObsWrapper cannot index this viewport");
+  if ((reinterpret_cast<uintptr_t>(features) & 15u) != 0)
+    return fail(WAB_E_INVALID, "wab_featurize: features must be 16-byte aligned");
+  const Params& p = h->p;
+  wab::FeatParams fp;
+  std::memset(&fp, 0, sizeof(fp));
+  fp.W = p.W; fp.H = p.H; fp.S = p.S; fp.OB = p.OB;
+  fp.md = p.W / 2 + p.H / 2 + 1;
+  fp.F = F;
+  fp.turns_empty = p.turns_empty;
+  fp.restrict_view = p.restrict_view;
+  fp.B = p.B;
+  std::memcpy(fp.mask_rows, p.mask_rows, sizeof(fp.mask_rows));
+  fp.planes = obs->planes;
+  fp.food_turns = obs->food_turns;
+  fp.role = obs->role;
+  fp.status = obs->status;
+  fp.view_mask = view_mask;
+  fp.out = features;
+  if (h->n_blocks == 0) return WAB_OK;
+  const uint32_t inW = (uint32_t)(64 * p.OB + 31) / 32, outW = (uint32_t)(64 * F + 31) / 32;
+  const size_t lds = (size_t)(((inW + 3) & ~3u) + outW) * 4;
+  DeviceGuard guard(h->device);
+  if (lds > 64 * 1024)
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<void*>(&wab::wab_featurize_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(wab::wab_featurize_kernel, dim3(h->n_blocks), dim3(256), lds, (hipStream_t)stream, fp);
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+
+int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, int64_t B, double gamma,
+                           const float* bootstrap, float* returns, void* stream) {
+  g_err.clear();
+  if (!reward || !done || !returns || T < 0 || B < 0)
+    return fail(WAB_E_INVALID, "wab_discounted_returns: bad argument");
+  if (T == 0 || B == 0) return WAB_OK;
+  hipLaunchKernelGGL(wab::wab_returns_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns);
+  HIP_TRY(hipGetLastError());
   return WAB_OK;
 }
 
