@@ -33,6 +33,16 @@ CONFIGS = {
 }
 
 
+def committed_traffic(config, batch):
+    """HBM bytes per launch from the PMC summary committed under profiles/ for this
+    workload (tools/profile.sh + tools/summarize_profile.py), or None."""
+    path = os.path.join(REPO, "profiles", "traffic_%s_b%d.json" % (config, batch))
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    return d.get("hbm_bytes_per_launch", {}).get("total_corrected"), os.path.relpath(path, REPO)
+
+
 def alg_bytes_per_env_step(W, H):
     """1 B action + 3*W*H u8 obs + 8 B scalars/reward/done + 2*36 B state."""
     return 3 * W * H + 81
@@ -78,9 +88,9 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from wab_gym_amd.shard import env_id_base, max_over_ranks, rank_info
+
+    rank, world, local = rank_info()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -91,7 +101,8 @@ def main():
 
     opts, stride, desc = CONFIGS[args.config]
     B, K, W = args.batch, args.steps, args.warmup
-    env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev, env_id_base=rank * B,
+    env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
+                                    env_id_base=env_id_base(rank, B),
                                     autoreset=True, validate_actions=False, plane_stride=stride)
     env.reset()
     gen = torch.Generator(device=dev)
@@ -144,10 +155,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stream_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     # per-launch kernel duration: HIP events bracketing each launch on its stream (not timed above)
     n_k = min(K, 200)
@@ -166,6 +174,7 @@ def main():
         alg = alg_bytes_per_env_step(Wv, Hv)
         achieved = alg * B / (kern_ms * 1e-3) / 1e9
         value = world * B * K / elapsed
+        traffic, traffic_src = committed_traffic(args.config, B)
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -183,7 +192,11 @@ def main():
                        "viewport": [Wv, Hv], "plane_stride": env.S, "launch": args.mode,
                        "parallelism": "independent env shards x%d (no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "alg_bytes_per_launch": alg * B,
                          "kernel": "wab_kernel<0,8> (fused step)", "kernel_us": round(kern_ms * 1e3, 3),
                          "alg_bytes_per_env_step": alg},
             "stream_us_per_step": round(stream_ms * 1e3 / K, 3),

@@ -1,0 +1,32 @@
+"""Multi-GPU sharding of the env batch: independent shards, no collective.
+
+Rank r of N owns global env ids [r*B, (r+1)*B).  Every random draw is keyed by the global
+id, so the union of the shards reproduces one batch of N*B envs exactly (tested).  The
+only collectives are out of the data path: a barrier around the timed region and a MAX
+reduction of the elapsed time (bench.py).
+"""
+from __future__ import annotations
+
+import os
+
+
+def rank_info():
+    """(rank, world, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def env_id_base(rank: int, batch_per_rank: int) -> int:
+    return rank * batch_per_rank
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """MAX of a per-rank float over the default process group (identity when not initialised)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
