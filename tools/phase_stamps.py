@@ -46,8 +46,8 @@ def main():
     L.wab_debug_set_stamps(env._h, st.data_ptr())
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
-    acc, spans = [], []
-    sub_acc = {k: [] for k in [(3, 7), (7, 8), (8, 9), (9, 10), (10, 11), (11, 12), (12, 4)]}
+    acc, spans, starts, ends, slow_acc = [], [], [], [], []
+    sub_acc = {k: [] for k in [(2, 7), (7, 8), (8, 9), (9, 3)]}
     for t in range(args.steps):
         st.zero_()
         env.step(torch.randint(0, env.n_actions, (B,), device="cuda:0", generator=g))
@@ -55,22 +55,33 @@ def main():
         if t < 20:
             continue
         s = st.cpu().numpy().astype(np.int64)
-        d = np.diff(s[:, :7], axis=1)  # phase intervals per block (10 ns ticks)
+        d = np.diff(s[:, :7], axis=1)  # phase intervals per block (10 ns ticks); order 0..6
         acc.append(d.mean(axis=0))
         spans.append(s[:, 6].max() - s[:, 0].min())
+        starts.append(np.percentile(s[:, 0] - s[:, 0].min(), [50, 90, 100]))
+        ends.append(np.percentile(s[:, 6] - s[:, 0].min(), [0, 50, 100]))
+        ordr = np.argsort(s[:, 6])
+        slow = ordr[-len(ordr) // 50:]
+        fast = ordr[: len(ordr) // 2]
+        slow_acc.append((d[slow].mean(axis=0), d[fast].mean(axis=0),
+                         np.bincount(slow % 8, minlength=8), slow[:8]))
         for (a0, a1) in sub_acc:
             sub_acc[(a0, a1)].append((s[:, a1] - s[:, a0]).mean())
     a = np.mean(acc, axis=0) * 10 / 1000
-    names = ["A: loads+LDS init", "A2: bitmap scroll", "B: keyed draws", "C: dynamics+stores",
-             "D/E: reset jobs", "F: expand+store"]
+    names = ["A: loads+LDS init", "A2: bitmap scroll", "B|C1: draws | dynamics", "C2|D: plane+stores | resets",
+             "E|F1: reset envs | obs stores", "F2: reset obs stores"]
     for n, v in zip(names, a):
         print("%-22s %7.2f us" % (n, v))
     print("%-22s %7.2f us (sum of block means)" % ("block total", a.sum()))
     print("%-22s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
+    print("block start offsets p50/p90/max (us):", np.round(np.mean(starts, axis=0) * 10 / 1000, 2))
+    print("block end times p0/p50/max (us):     ", np.round(np.mean(ends, axis=0) * 10 / 1000, 2))
+    print("slowest 2%% blocks, per phase (us):", np.round(np.mean([a for a, _, _, _ in slow_acc], axis=0) * 10 / 1000, 2))
+    print("fastest 50%% blocks, per phase (us):", np.round(np.mean([b for _, b, _, _ in slow_acc], axis=0) * 10 / 1000, 2))
+    print("slowest blocks by blockIdx%%8:", np.sum([c for _, _, c, _ in slow_acc], axis=0))
+    print("example slow block ids:", slow_acc[-1][3])
     # phase C detail: 3 -> 7 -> 8 -> 9 -> 10 -> 11 -> 12 -> 4
-    sub = [("C1: log scan", 3, 7), ("C2: bitmap->plane", 7, 8), ("C3: wolves", 8, 9),
-           ("C4: eat", 9, 10), ("C5: starve+spawn", 10, 11), ("C6: reward", 11, 12),
-           ("C7: jobs+stores", 12, 4)]
+    sub = [("C1a: log", 2, 7), ("C1b: wolves", 7, 8), ("C1c: eat", 8, 9), ("C1d: rest+jobs", 9, 3)]
     for n, a0, a1 in sub:
         v = np.mean(sub_acc[(a0, a1)]) * 10 / 1000
         print("  %-20s %7.2f us" % (n, v))

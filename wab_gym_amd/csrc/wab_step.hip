@@ -50,8 +50,12 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// episode key = mix64(env_key ^ episode), env_key = mix64(mix64(seed + golden) ^ env)
+__device__ __forceinline__ uint64_t env_key(uint64_t seed, uint64_t env) {
+  return mix64(mix64(seed + 0x9E3779B97F4A7C15ull) ^ env);
+}
 __device__ __forceinline__ uint64_t episode_key(uint64_t seed, uint64_t env, uint64_t ep) {
-  return mix64(mix64(mix64(seed + 0x9E3779B97F4A7C15ull) ^ env) ^ ep);
+  return mix64(env_key(seed, env) ^ ep);
 }
 
 __device__ __forceinline__ uint32_t make_ts(uint32_t site, uint32_t k, int32_t turn) {
@@ -78,14 +82,24 @@ __device__ __forceinline__ uint64_t draw_U(uint32_t xy, uint32_t ts, uint32_t b0
 }
 
 // number of thresholds T_k <= U: the reference's round(u**power * max) (wab_env.py:631-635);
-// `thr` is the LDS copy of the table
+// `thr` is the LDS copy of the sorted table (n <= 255).  16-ary search in two levels of
+// independent LDS reads (two round trips instead of log2(n) dependent ones).
 __device__ __forceinline__ int bush_value(const uint64_t* thr, int n, uint64_t U) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (thr[mid] <= U) lo = mid + 1; else hi = mid;
+  const int step = (n + 15) >> 4;  // <= 16
+  int c = 0;
+#pragma unroll
+  for (int i = 1; i < 16; ++i) {
+    const int k = i * step - 1;
+    c += (k < n && thr[k] <= U) ? 1 : 0;
   }
-  return lo;
+  const int base = c * step;
+  int c2 = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = base + j;
+    c2 += (j < step && k < n && thr[k] <= U) ? 1 : 0;
+  }
+  return base + c2;
 }
 
 // packed-tile add: both int16 halves wrap independently (v_pk_add_u16)
@@ -222,7 +236,14 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
   int32_t ox = 0, oy = 0, turn = 0, role = 0, status = 0, nw = 0, ne = 0, ndep = 0, dir = DIR_STAY;
   double food = 0.0, reward = 0.0;
   uint32_t ep = 0, b0 = 0, b1 = 0;
+  uint64_t ek_next = 0;  // key of the episode an auto-reset would start
   bool done = false;
+  // eaten-log prefetch (phase A -> C): the first kLogPrefetch entries, when needed
+  constexpr int kLogPrefetch = 4;
+  uint32_t lxy[kLogPrefetch], lrem[kLogPrefetch];
+#pragma unroll
+  for (int i = 0; i < kLogPrefetch; ++i) { lxy[i] = 0u; lrem[i] = 0u; }
+  bool need_log = false;
   unsigned long long bad = 0, eaten_of = 0, wolf_of = 0;
   // wolves of this env: slot registers + a live mask (slot order is irrelevant: co-located
   // wolves are interchangeable, so only the multiset of positions is state)
@@ -237,6 +258,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
     // every load is independent and issued up front: one memory round trip
     const uint4 hdr = p.hdr[g];
     const int a = (int)p.actions[g];
+    const uint64_t kenv = env_key(p.seed, (uint64_t)(p.env_base + g));  // overlaps the loads
     food = p.food[g];
     const uint32_t w0 = p.wolves[g], w1 = p.wolves[p.B + g];  // slots 0, 1 speculatively
     uint32_t bmr[4] = {0u, 0u, 0u, 0u};
@@ -286,9 +308,25 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
         if (k < NWd) BM<NE>(bm, k, e) = v[k];
       }
     }
-    const uint64_t ek = episode_key(p.seed, (uint64_t)(p.env_base + g), ep);
+    const uint64_t ek = mix64(kenv ^ (uint64_t)ep);
+    ek_next = mix64(kenv ^ (uint64_t)(ep + 1u));
     b0 = (uint32_t)ek;
     b1 = (uint32_t)(ek >> 32);
+    // eaten log: needed for the berries on the ostrich's tile, or for emptied tiles that may
+    // scroll back into view; issued now, consumed in phase C (latency hidden by phase B)
+    {
+      const uint32_t ccb = (uint32_t)(p.cw * p.H + p.ch);
+      const bool center = SMALL ? ((BM<NE>(bm, ccb >> 5, e) >> (ccb & 31)) & 1u) != 0u : true;
+      const bool center_in_strip = (dir == DIR_RIGHT || dir == DIR_LEFT) ? p.W == 1
+                                   : (dir == DIR_UP || dir == DIR_DOWN) ? p.H == 1 : false;
+      need_log = ne > 0 && (center || center_in_strip || (ndep > 0 && dir != DIR_STAY));
+#pragma unroll
+      for (int i = 0; i < kLogPrefetch; ++i)
+        if (need_log && i < ne) {
+          lxy[i] = p.eaten_xy[(int64_t)i * p.B + g];
+          lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
+        }
+    }
     uint4 sn;
     sn.x = xy_pack(ox, oy);
     sn.y = b0;
@@ -423,12 +461,20 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       const bool center_bush = (BM<NE>(bm, ccb >> 5, e) >> (ccb & 31)) & 1u;
       // eaten-tile log, read only when it can matter: for the berries left on the ostrich's
       // tile, and for emptied tiles that may have scrolled back into view (absent from S, :506)
-      int found = -1;
-      if (center_bush || (ndep > 0 && dir != DIR_STAY)) {
+      int found = -1, found_rem = 0;
+      if (need_log && (center_bush || (ndep > 0 && dir != DIR_STAY))) {
         for (int i = 0; i < ne; ++i) {
-          const uint32_t v = p.eaten_xy[(int64_t)i * p.B + g];
-          const int r = (int)p.eaten_rem[(int64_t)i * p.B + g];
-          if (v == cpos) found = i;
+          uint32_t v = 0;
+          int r = 0;
+          if (i < kLogPrefetch) {
+#pragma unroll
+            for (int q = 0; q < kLogPrefetch; ++q)
+              if (q == i) { v = lxy[q]; r = (int)lrem[q]; }
+          } else {
+            v = p.eaten_xy[(int64_t)i * p.B + g];
+            r = (int)p.eaten_rem[(int64_t)i * p.B + g];
+          }
+          if (v == cpos) { found = i; found_rem = r; }
           const int ddx = ox - xy_x(v), ddy = oy - xy_y(v);
           if (r == 0 && abs(ddx) <= p.cw && abs(ddy) <= p.ch) {
             const uint32_t cb = (uint32_t)((ddx + p.cw) * p.H + ddy + p.ch);
@@ -475,7 +521,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       // berries left on the ostrich's tile: eaten log, else the tile's generated value
       int rem;
       if (found >= 0)
-        rem = p.eaten_rem[(int64_t)found * p.B + g];
+        rem = found_rem;
       else if (center_bush)
         rem = bush_value(thr, p.max_berries, draw_U(cpos, make_ts(SITE_BUSH, 0, 0), b0, b1));
       else
@@ -562,7 +608,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       // reset (:231-248, spawn_ostriches :595-611)
       const int j = __popcll(jm & ((1ull << e) - 1ull));
       ep += 1u;  // 0xFFFFFFFF -> 0 on the first reset
-      const uint64_t ek = episode_key(p.seed, (uint64_t)(p.env_base + g), ep);
+      const uint64_t ek = MODE == MODE_STEP ? ek_next : episode_key(p.seed, (uint64_t)(p.env_base + g), ep);
       b0 = (uint32_t)ek;
       b1 = (uint32_t)(ek >> 32);
       jobEnv[j] = (uint32_t)e;
