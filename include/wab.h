@@ -169,6 +169,10 @@ int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* 
 /* Batch size of a handle. */
 int64_t wab_batch(const wab_handle* h);
 
+/* Name of the kernel wab_step launches for this handle ("small": the four-wave kernel for
+ * views of at most 128 cells; "block": the general one).  Diagnostics only. */
+const char* wab_step_kernel(const wab_handle* h);
+
 /* ---- config 5 (actor_critic.py rollout) ------------------------------------------ */
 
 /* Length of the flattened PragmaticObsWrapper observation for the handle's options

@@ -41,11 +41,14 @@ def main():
     L = _lib.load()
     L.wab_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     nb = (B + 63) // 64
-    st = torch.zeros((nb, 16), dtype=torch.int64, device="cuda:0")
+    st = torch.zeros((nb, 32), dtype=torch.int64, device="cuda:0")
     env.reset()
     L.wab_debug_set_stamps(env._h, st.data_ptr())
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
+    kind = os.environ.get("WAB_STEP_KERNEL", "small")
+    if kind != "block":
+        return small_report(env, st, g, args.steps)
     acc, spans, starts, ends, slow_acc = [], [], [], [], []
     sub_acc = {k: [] for k in [(2, 7), (7, 8), (8, 9), (9, 3)]}
     for t in range(args.steps):
@@ -85,6 +88,46 @@ def main():
     for n, a0, a1 in sub:
         v = np.mean(sub_acc[(a0, a1)]) * 10 / 1000
         print("  %-20s %7.2f us" % (n, v))
+
+
+def small_report(env, st, g, steps):
+    """wab_step_small: W0 stamps 0..9, W1 10..15, W2 16..21, W3 22..27 (SMALL_STAMP)."""
+    import numpy as np
+    import torch
+
+    B = env.num_envs
+    nb = (B + 63) // 64
+    waves = {"W0 bushes": ([0, 1, 2, 7, 8, 3, 4, 5, 6],
+                           ["loads, scroll, key", "strip draws", "eaten log", "tile value (W1)", "eat, starve",
+                            "B1 + status, scalars, bushes", "B2 (+ terminal obs)", "obs stores"]),
+             "W1 value + ring A": ([10, 11, 12, 13, 14, 15], ["loads, thresholds, tile value", "ring A",
+                                                               "B1 + render S", "B2", "obs stores"]),
+             "W2 wolves": ([16, 17, 18, 19, 20, 21], ["loads, despawn, pursuit", "ring B",
+                                                       "B1 + spawns, slots, header", "B2", "obs stores"]),
+             "W3 ring C": ([22, 23, 25, 26, 27], ["loads, ring C", "B1 + reset draws, new episodes", "B2",
+                                                   "obs stores"])}
+    acc = {k: [] for k in waves}
+    spans, ends = [], []
+    for t in range(steps):
+        st.zero_()
+        env.step(torch.randint(0, env.n_actions, (B,), device="cuda:0", generator=g))
+        torch.cuda.synchronize()
+        if t < 20:
+            continue
+        s = st.cpu().numpy().astype(np.int64)[:nb]
+        t0 = min(s[:, 0].min(), s[:, 10].min(), s[:, 16].min(), s[:, 22].min())
+        for k, (cols, _) in waves.items():
+            acc[k].append(np.diff(s[:, cols], axis=1).mean(axis=0))
+        end = s[:, [6, 15, 21, 27]].max(axis=1)
+        spans.append(end.max() - t0)
+        ends.append(np.percentile(end - t0, [0, 50, 100]))
+    for k, (cols, names) in waves.items():
+        a = np.mean(acc[k], axis=0) * 10 / 1000
+        print("%s:" % k)
+        for n, v in zip(names, a):
+            print("  %-28s %7.2f us" % (n, v))
+    print("%-24s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
+    print("workgroup end times p0/p50/max (us):", np.round(np.mean(ends, axis=0) * 10 / 1000, 2))
 
 
 if __name__ == "__main__":

@@ -6,6 +6,7 @@ before comparing with a byte count; WRITE_SIZE is exact for 16-byte-per-lane sto
 obs stores).  Usage: python tools/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag>
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -14,10 +15,10 @@ import sys
 
 def kernel_rows(path, kernel):
     rows = list(csv.DictReader(open(path)))
-    return [r for r in rows if kernel in r["Kernel_Name"]]
+    return [r for r in rows if re.search(kernel, r["Kernel_Name"])]
 
 
-def main(src, dst, kernel="wab_kernel<0"):
+def main(src, dst, kernel=r"wab_kernel<0|wab_step_q4"):
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
@@ -26,7 +27,7 @@ def main(src, dst, kernel="wab_kernel<0"):
             shutil.copy(os.path.join(src, log), os.path.join(dst, log))
     summ = {"kernel": kernel}
     for r in csv.DictReader(open(stats)):
-        if kernel in r["Name"]:
+        if re.search(kernel, r["Name"]):
             summ["trace"] = {"name": r["Name"], "calls": int(r["Calls"]),
                              "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
                              "max_ns": float(r["MaxNs"])}

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("WAB_LIB") or os.path.join(HERE, "_lib", "libwab_hip.s
 EXPORTED = [
     "wab_abi_version", "wab_last_error", "wab_num_actions", "wab_create", "wab_destroy",
     "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
-    "wab_feature_dim", "wab_featurize", "wab_discounted_returns",
+    "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
 ]
 
 ABI_VERSION = 1
@@ -68,8 +68,10 @@ def load():
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64
+    L.wab_step_kernel.argtypes = [P]
+    L.wab_step_kernel.restype = ctypes.c_char_p
     for name in EXPORTED:
-        if name not in ("wab_abi_version", "wab_last_error", "wab_batch"):
+        if name not in ("wab_abi_version", "wab_last_error", "wab_batch", "wab_step_kernel"):
             getattr(L, name).restype = ctypes.c_int
     if L.wab_abi_version() != ABI_VERSION:
         raise WabError("libwab_hip.so ABI %d != %d" % (L.wab_abi_version(), ABI_VERSION))

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -17,6 +18,8 @@
 namespace wab {
 template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
+template <int SLOTS>
+__global__ void wab_step_small(Params p);
 
 struct FeatParams {
   int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
@@ -42,6 +45,8 @@ struct wab_handle {
   int slots = 8;
   int n_blocks = 0;
   size_t lds_bytes = 0;
+  int step_kernel = 0;         // KERNEL_BLOCK / KERNEL_SMALL
+  size_t small_lds_bytes = 0;  // LDS of the small-view kernel
   bool reset_done = false;
   std::vector<void*> allocs;
 };
@@ -113,10 +118,35 @@ void launch_as(wab_handle* h, const Params& p, hipStream_t stream) {
 // SMALL: the W*H-bit view bitmap fits 4 registers (default 11x11 = 121 bits)
 bool small_map(const Params& p) { return p.WHW <= 4; }
 
+// Step kernels.  The block kernel (wab_step.hip) handles every configuration; views whose
+// planes fit 128 bits (W*H <= 128, unpadded rows, spawn ring <= 128 tiles, restrict_view only
+// at exactly 11x11) step with the four-wave small-view kernel (wab_step_small.hip).
+// WAB_STEP_KERNEL=block selects the block kernel for those too (A/B measurements).
+enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1 };
+
+bool small_view(const Params& p) {
+  return p.WH <= 128 && p.S == p.H && p.R <= 128 && (!p.restrict_view || (p.W == 11 && p.H == 11));
+}
+
+void* small_kernel_ptr(int slots) {
+  switch (slots) {
+    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16>);
+    default: return reinterpret_cast<void*>(&wab::wab_step_small<32>);
+  }
+}
+
 template <int MODE>
 int launch(wab_handle* h, const Params& p, hipStream_t stream) {
   if (h->n_blocks == 0) return WAB_OK;
-  if (small_map(p)) launch_as<MODE, true>(h, p, stream);
+  if (MODE == 0 && h->step_kernel == KERNEL_SMALL) {
+    const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
+    switch (h->slots) {
+      case 8: hipLaunchKernelGGL(wab::wab_step_small<8>, grid, block, h->small_lds_bytes, stream, p); break;
+      case 16: hipLaunchKernelGGL(wab::wab_step_small<16>, grid, block, h->small_lds_bytes, stream, p); break;
+      default: hipLaunchKernelGGL(wab::wab_step_small<32>, grid, block, h->small_lds_bytes, stream, p); break;
+    }
+  } else if (small_map(p)) launch_as<MODE, true>(h, p, stream);
   else launch_as<MODE, false>(h, p, stream);
   HIP_TRY(hipGetLastError());
   return WAB_OK;
@@ -153,6 +183,11 @@ const char* wab_last_error(void) { return g_err.c_str(); }
 int wab_num_actions(const wab_config* cfg) { return cfg ? n_actions_of(cfg) : WAB_E_INVALID; }
 
 int64_t wab_batch(const wab_handle* h) { return h ? h->p.B : 0; }
+
+const char* wab_step_kernel(const wab_handle* h) {
+  if (!h) return "";
+  return h->step_kernel == KERNEL_SMALL ? "small" : "block";
+}
 
 int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id_base, int device,
                wab_handle** out) {
@@ -203,12 +238,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   p.SL = p.W > p.H ? p.W : p.H;
   p.magic_OB = (uint32_t)((1ull << 32) / (uint64_t)p.OB) + 1u;
   p.n_actions = n_actions_of(c);
-  static const int dx[6] = {0, 1, 0, -1, 0, 0}, dy[6] = {1, 0, -1, 0, 0, 0};  // up right down left
-  for (int a = 0; a < 6; ++a) {
-    p.act_dx[a] = dx[a];
-    p.act_dy[a] = dy[a];
-    p.act_role[a] = -1;
-  }
+  for (int a = 0; a < 6; ++a) p.act_role[a] = -1;  // moves: wab::decode_action (up right down left)
   if (c->gatherer_only) p.act_role[4] = 1;       // wab_env.py:149-159
   else if (c->lookout_only) p.act_role[4] = 0;   // :160-170
   else { p.act_role[4] = 1; p.act_role[5] = 0; } // :171-182
@@ -249,6 +279,11 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     if (j == 0) p.small_masks[0][c >> 5] |= 1u << (c & 31);
     if (j == p.H - 1) p.small_masks[1][c >> 5] |= 1u << (c & 31);
   }
+  if (p.W == 11 && p.H == 11)
+    for (int r = 0; r < 2; ++r)
+      for (int i = 0; i < 11; ++i)
+        for (int j = 0; j < 11; ++j)
+          if ((p.mask_rows[r][i] >> j) & 1u) p.view121[r][(i * 11 + j) >> 5] |= 1u << ((i * 11 + j) & 31);
   p.seed = seed;
   p.env_base = env_id_base;
   p.B = batch;
@@ -257,6 +292,11 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   h->slots = slots;
   h->n_blocks = (int)((batch + wab::kEnvsPerBlock - 1) / wab::kEnvsPerBlock);
   h->lds_bytes = (size_t)wab::lds_layout(p, slots).total * 4u;
+  {
+    const char* k = std::getenv("WAB_STEP_KERNEL");
+    h->step_kernel = small_view(p) && !(k && std::strcmp(k, "block") == 0) ? KERNEL_SMALL : KERNEL_BLOCK;
+    h->small_lds_bytes = (size_t)wab::small_layout(p).total * 4u;
+  }
   if (h->lds_bytes > 160u * 1024u) {
     delete h;
     return fail(WAB_E_INVALID, "viewport too large for the fused kernel's LDS budget");
@@ -282,14 +322,38 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   uint64_t* thr = nullptr;
   rc |= alloc((void**)&thr, (size_t)(p.max_berries > 0 ? p.max_berries : 1) * 8);
+  uint32_t* tab = nullptr;
+  p.ring_at = (p.WH + 3) & ~3;
+  const int n_tab = p.ring_at + ((p.R + 3) & ~3) + 4;  // + the kernel's one-ahead prefetch
+  rc |= alloc((void**)&tab, (size_t)n_tab * 4);
   if (rc != WAB_OK) {
     std::string msg = g_err;
     wab_destroy(h);
     return fail(WAB_E_NOMEM, msg);
   }
   p.thresholds = thr;
+  p.tables = tab;
   hipError_t e = hipSuccess;
-  if (p.max_berries > 0)
+  {  // view-cell offsets (cw - i, ch - j) for cell i*H + j, then the spawn-ring offsets
+    std::vector<uint32_t> t((size_t)n_tab, 0u);
+    for (int c = 0; c < p.WH; ++c) t[c] = wab::xy_pack(p.cw - c / p.H, p.ch - c % p.H);
+    const int m = p.margin, Wm = p.W + 2 * m;
+    for (int r = 0; r < p.R; ++r) {
+      int xi, yi;
+      if (r < 2 * m * Wm) {
+        const int band = r / Wm;
+        xi = r % Wm;
+        yi = band < m ? band : band + p.H;
+      } else {
+        const int r2 = r - 2 * m * Wm, band = r2 / p.H;
+        yi = m + r2 % p.H;
+        xi = band < m ? band : band + p.W;
+      }
+      t[p.ring_at + r] = wab::xy_pack(xi - p.cw - m, yi - p.ch - m);
+    }
+    e = hipMemcpy(tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess && p.max_berries > 0)
     e = hipMemcpy(thr, c->bush_thresholds, (size_t)p.max_berries * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess && B > 0) {  // every env: episode 0xFFFFFFFF (the first reset makes it 0)
     std::vector<uint4> init(B, make_uint4(0u, 0u, 0u, 0xFFFFFFFFu));
@@ -301,6 +365,9 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
                   kernel_ptr<1, false>(slots)})
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
+  if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
+    e = hipFuncSetAttribute(small_kernel_ptr(slots), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)h->small_lds_bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     std::string msg = std::string("wab_create: ") + hipGetErrorString(e);

@@ -1,0 +1,182 @@
+// wab_device.h — device helpers shared by the step kernels (wab_step.hip, wab_step_q4.hip):
+// the keyed RNG (definition: oracle/keyed_rng.py), threshold search, packed tiles, LDS bit ops.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "wab_params.h"
+
+namespace wab {
+
+enum : uint32_t { SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5 };
+enum { MODE_STEP = 0, MODE_RESET = 1 };
+enum { DIR_STAY = 0, DIR_RIGHT = 1, DIR_LEFT = 2, DIR_UP = 3, DIR_DOWN = 4 };
+
+// ------------------------------------------------------------------------ keyed RNG
+// Definition: oracle/keyed_rng.py (the golden vectors were generated under it).
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// episode key = mix64(env_key ^ episode), env_key = mix64(mix64(seed + golden) ^ env)
+__device__ __forceinline__ uint64_t env_key(uint64_t seed, uint64_t env) {
+  return mix64(mix64(seed + 0x9E3779B97F4A7C15ull) ^ env);
+}
+__device__ __forceinline__ uint64_t episode_key(uint64_t seed, uint64_t env, uint64_t ep) {
+  return mix64(env_key(seed, env) ^ ep);
+}
+
+__device__ __forceinline__ uint32_t make_ts(uint32_t site, uint32_t k, int32_t turn) {
+  return (site & 0xFu) | ((k & 0xFFu) << 4) | (((uint32_t)turn & 0xFFFFFu) << 12);
+}
+
+__device__ __forceinline__ uint32_t draw_lo21(uint32_t h1, uint32_t ts, uint32_t b0) {
+  const uint32_t rot = (ts << 16) | (ts >> 16);
+  return fmix32(h1 ^ rot ^ b0 ^ 0x9E3779B9u) >> 11;
+}
+
+// U >= T for U = hi << 21 | lo21 and T = th << 21 | tl; the low half is only hashed when
+// the high 32 bits tie (probability 2^-32)
+__device__ __forceinline__ bool U_ge(uint32_t h1, uint32_t hi, uint32_t ts, uint32_t b0, uint32_t th,
+                                     uint32_t tl) {
+  if (hi != th) return hi > th;
+  return draw_lo21(h1, ts, b0) >= tl;
+}
+
+__device__ __forceinline__ uint64_t draw_U(uint32_t xy, uint32_t ts, uint32_t b0, uint32_t b1) {
+  const uint32_t h1 = fmix32(xy ^ b0);
+  const uint32_t hi = fmix32(h1 ^ ts ^ b1);
+  return ((uint64_t)hi << 21) | draw_lo21(h1, ts, b0);
+}
+
+// number of thresholds T_k <= U: the reference's round(u**power * max) (wab_env.py:631-635);
+// `thr` is the LDS copy of the sorted table (n <= 255).  16-ary search in two levels of
+// independent LDS reads (two round trips instead of log2(n) dependent ones).
+__device__ __forceinline__ int bush_value(const uint64_t* thr, int n, uint64_t U) {
+  const int step = (n + 15) >> 4;  // <= 16
+  int c = 0;
+#pragma unroll
+  for (int i = 1; i < 16; ++i) {
+    const int k = i * step - 1;
+    c += (k < n && thr[k] <= U) ? 1 : 0;
+  }
+  const int base = c * step;
+  int c2 = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = base + j;
+    c2 += (j < step && k < n && thr[k] <= U) ? 1 : 0;
+  }
+  return base + c2;
+}
+
+// packed-tile add: both int16 halves wrap independently (v_pk_add_u16)
+typedef unsigned short wab_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t xy_add(uint32_t a, uint32_t b) {
+  wab_u16x2 va = __builtin_bit_cast(wab_u16x2, a), vb = __builtin_bit_cast(wab_u16x2, b);
+  return __builtin_bit_cast(uint32_t, va + vb);
+}
+
+__device__ __forceinline__ uint32_t udiv(uint32_t x, uint32_t d, uint32_t magic) {
+  uint32_t q = __umulhi(x, magic);
+  const int32_t r = (int32_t)(x - q * d);
+  if (r < 0) q -= 1; else if ((uint32_t)r >= d) q += 1;
+  return q;
+}
+
+__device__ __forceinline__ void lds_set(uint32_t* s, uint32_t bit) { atomicOr(&s[bit >> 5], 1u << (bit & 31)); }
+
+// OR the low `nbits` (<= 32) bits of v into the stream at bit offset `at`
+__device__ __forceinline__ void lds_or_bits(uint32_t* s, uint32_t at, uint32_t v, uint32_t nbits) {
+  if (nbits < 32) v &= (1u << nbits) - 1u;
+  if (!v) return;
+  const uint64_t m = (uint64_t)v << (at & 31);
+  atomicOr(&s[at >> 5], (uint32_t)m);
+  if (m >> 32) atomicOr(&s[(at >> 5) + 1], (uint32_t)(m >> 32));
+}
+
+// restrict_view: zero blind-spot cells of the three planes (mask_grid, wab_env.py:344-357)
+__device__ __forceinline__ void apply_view_mask(const Params& p, uint32_t* s, uint32_t env_bit, int role) {
+  const uint32_t* rows = p.mask_rows[role == 1 ? 1 : 0];
+  for (int pl = 0; pl < 3; ++pl)
+    for (int i = 0; i < 11; ++i) {
+      const uint32_t base = env_bit + (uint32_t)(pl * p.W * p.S + i * p.S);
+      const uint64_t m = (uint64_t)rows[i] << (base & 31);
+      atomicAnd(&s[base >> 5], ~(uint32_t)m);
+      if (m >> 32) atomicAnd(&s[(base >> 5) + 1], ~(uint32_t)(m >> 32));
+    }
+}
+
+// 128-bit shifts of a W*H <= 128 bitmap held as two 64-bit halves
+__device__ __forceinline__ void shl128(uint64_t& lo, uint64_t& hi, int n) {
+  if (n >= 64) { hi = lo << (n - 64); lo = 0; }
+  else if (n > 0) { hi = (hi << n) | (lo >> (64 - n)); lo <<= n; }
+}
+__device__ __forceinline__ void shr128(uint64_t& lo, uint64_t& hi, int n) {
+  if (n >= 64) { lo = hi >> (n - 64); hi = 0; }
+  else if (n > 0) { lo = (lo >> n) | (hi << (64 - n)); hi >>= n; }
+}
+
+// Pin a wave-uniform value (a kernel-argument field) to scalar registers.  A per-lane
+// select between two kernel-argument fields otherwise compiles to a select of their
+// addresses and a vector load from the kernarg segment, whose s_waitcnt vmcnt then also
+// waits for every store the wave has in flight.
+__device__ __forceinline__ uint32_t sreg(uint32_t v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ int32_t sreg(int32_t v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ double sreg(double v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+// Per-lane choice between two wave-uniform 64-bit values by masks: the compiler turns a
+// plain ?: of two kernel-argument doubles into a scratch array indexed per lane.
+__device__ __forceinline__ uint64_t sel64(bool c, uint64_t a, uint64_t b) {
+  const uint64_t m = 0ull - (uint64_t)c;
+  return (a & m) | (b & ~m);
+}
+__device__ __forceinline__ double sel_f64(bool c, double a, double b) {
+  return __longlong_as_double((long long)sel64(c, (uint64_t)__double_as_longlong(a), (uint64_t)__double_as_longlong(b)));
+}
+
+// The action table (wab_env.py:149-182: 0 up, 1 right, 2 down, 3 left, 4/5 role actions),
+// decoded arithmetically: indexing the kernel-argument block with a per-lane value compiles
+// to a vector load from the kernarg segment, a dependent memory round trip per step.
+__device__ __forceinline__ void decode_action(const Params& p, int a, int& dx, int& dy, int& new_role) {
+  dx = (a == 1) - (a == 3);
+  dy = (a == 0) - (a == 2);
+  const int32_t r4 = sreg(p.act_role[4]), r5 = sreg(p.act_role[5]);
+  new_role = a == 4 ? r4 : a == 5 ? r5 : -1;
+}
+
+__device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
+
+// Workgroup barrier for LDS hand-offs only.  Waves of a block exchange data exclusively
+// through LDS; __syncthreads() would also drain every outstanding global store
+// (s_waitcnt vmcnt(0)) and put HBM write latency on the critical path of each phase.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// tile-table entry: world offset from the ostrich (int8, int8) and a bit index
+__device__ __forceinline__ int tile_dx(uint32_t t) { return (int)(int8_t)(t & 0xFFu); }
+__device__ __forceinline__ int tile_dy(uint32_t t) { return (int)(int8_t)((t >> 8) & 0xFFu); }
+__device__ __forceinline__ uint32_t tile_bit(uint32_t t) { return t >> 16; }
+
+}  // namespace wab

@@ -43,13 +43,15 @@ struct Params {
   uint32_t magic_OB;        // floor(2^32 / OB) + 1 (division helper)
   // ---- rules
   int32_t n_actions;
-  int32_t act_dx[6], act_dy[6], act_role[6];  // role -1 = NaN (unchanged)
+  int32_t act_role[6];      // role set by each action, -1 = NaN (unchanged); moves: decode_action()
   // "U >= T" tests on 53-bit draws U = hi << 21 | lo21, split as (T >> 21, T & 0x1FFFFF);
   // T = 2^53 ("never") is encoded (0xFFFFFFFF, 0xFFFFFFFF) which no (hi, lo21) reaches
   uint32_t keep_th, keep_tl;    // despawn: wolf kept iff U >= keep_gt + 1  (u > p, wab_env.py:263)
   uint32_t spawn_th, spawn_tl;  // spawn: wolf iff !(U >= spawn_lt)          (u < p/2, wab_env.py:573)
   uint32_t bush_th, bush_tl;    // bush present iff U >= T_1                 (wab_env.py:632-635)
   const uint64_t* thresholds;  // device [max_berries] T_k
+  const uint32_t* tables;      // device: [WH] view-cell world offsets (cw - i, ch - j), then from
+  int32_t ring_at;             //   ring_at (16-B aligned) the R ring offsets, padded to a multiple of 4
   int32_t max_berries;
   double fill, hunger;
   double r_turn, r_killed, r_starve, r_finish, r_eat;
@@ -59,6 +61,7 @@ struct Params {
   int32_t lookout_only, restrict_view, wolves_on, wolves_can_move, god_mode, autoreset;
   uint32_t mask_rows[2][11];  // restrict_view: 11-bit row masks per role (bit j <=> mask[i][j])
   uint32_t small_masks[3][4]; // W*H <= 128: column 0, column H-1, valid-bit masks of the bitmap
+  uint32_t view121[2][4];     // restrict_view at 11x11: the row masks as one 121-bit plane mask
   // ---- identity
   uint64_t seed;
   int64_t env_base;
@@ -113,6 +116,33 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) 
   L.jobKey = o; o += 2u * NE;
   L.blk = o; o += 4u;
   L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
+  L.total = o;
+  return L;
+}
+
+// LDS of the four-wave small-view step (wab_step_small.hip): one 64-env group per
+// workgroup (dwords)
+struct SmallLayout {
+  uint32_t tiles, thr, stream, stream_words, cval, flag, wolfp, kill, bushp, info, spawn, jbm, jwm, jkey, total;
+};
+
+__host__ __device__ inline SmallLayout small_layout(const Params& p) {
+  SmallLayout L;
+  uint32_t o = 0;
+  L.tiles = o; o += lds_align4((uint32_t)p.WH);
+  L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
+  L.stream_words = lds_align4((64u * (uint32_t)p.OB + 31u) >> 5);
+  L.stream = o; o += L.stream_words + 4u;  // + slack for stream_or128's fifth dword
+  L.cval = o; o += 64u;
+  L.flag = o; o += 4u;
+  L.wolfp = o; o += 64u * 4u;
+  L.kill = o; o += 64u;
+  L.bushp = o; o += 64u * 4u;
+  L.info = o; o += 64u;
+  L.spawn = o; o += 3u * 64u * 4u;
+  L.jbm = o; o += 64u * 4u;
+  L.jwm = o; o += 64u * 4u;  // (directly after jbm: zeroed together)
+  L.jkey = o; o += 2u * 64u;
   L.total = o;
   return L;
 }

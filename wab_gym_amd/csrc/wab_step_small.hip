@@ -1,0 +1,789 @@
+// wab_step_small.hip — the fused step for small views (W*H <= 128 bits, S == H, spawn ring
+// <= 128 tiles; the default 11x11 options).
+//
+// The step is latency-bound, not throughput-bound: a lone wave issues at best one instruction
+// every ~4-5 cycles (twice that along a dependent chain; tools/micro/valu_latency.hip), and
+// the kernel at batch 4096 takes nearly as long as at 65536 (SQ_WAIT_ANY ~70 % of wave
+// cycles).  What shortens the step is cutting the longest per-env dependency chain.  Each
+// 64-env group (one env per lane) is served by four waves of one 256-thread workgroup, each
+// running an independent part of the step; they meet at four LDS barriers:
+//
+//          W0 bushes             W1 draws             W2 wolves             W3 ring
+//   P0     loads, scroll,        entering row/col     despawn, pursuit,     thresholds, the
+//          first log entries     draws                kill; ring part A     ostrich tile value
+//   -- B0 --
+//   P1     rest of the log,      ring part B          ring part C           ring part D
+//          eat, hunger, starve
+//   -- B1 --
+//   P2     status, reward,       render S             spawns, wolf slots    reset draws of
+//          done, scalars                                                    the done envs
+//   -- B2 --
+//   P3     state stores, new episodes of the done envs
+//   -- B3 --  all: obs bit-stream -> bytes, 16-byte stores
+//
+// Every wave that needs "done" recomputes it from the flags handed over at B1 (starved from
+// W0, killed from W2), so no wave waits for another's bookkeeping.  Draws are batched four
+// at a time (fmix32x4) so dependent hash chains interleave; the rare threshold ties (high
+// 32 bits equal) are resolved in a separate branch.
+#include <hip/hip_runtime.h>
+
+#include "wab_small.h"
+
+namespace wab {
+
+// Diagnostic build (-DWAB_STAMPS): lane 0 of each wave records s_memrealtime (100 MHz) at
+// phase boundaries into p.stamps[workgroup * 32 + slot] (W0 0..9, W1 10..15, W2 16..21, W3 22..27):
+// a wave's stamps k, k+1, k+2, k+3 close its phases P0..P3 (the barrier waits sit at the
+// start of the next phase), the last one the retirement of its obs stores.
+#ifdef WAB_STAMPS
+#define SMALL_STAMP(slot)                                                                \
+  do {                                                                                   \
+    if (lane == 0 && p.stamps)                                                           \
+      p.stamps[(size_t)blockIdx.x * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#else
+#define SMALL_STAMP(slot) do {} while (0)
+#endif
+
+namespace {
+
+__device__ __forceinline__ void set_bit_if(M128& m, uint32_t c, bool on) {
+  const uint64_t b = on ? 1ull << (c & 63u) : 0ull;
+  m.lo |= c < 64u ? b : 0ull;
+  m.hi |= c < 64u ? 0ull : b;
+}
+__device__ __forceinline__ uint4 m_pack(const M128& m) {
+  return make_uint4((uint32_t)m.lo, (uint32_t)(m.lo >> 32), (uint32_t)m.hi, (uint32_t)(m.hi >> 32));
+}
+__device__ __forceinline__ M128 m_unpack(const uint4& v) { return m_make(v.x, v.y, v.z, v.w); }
+
+// The part of the state every wave reads: header and action, the move (:252-258), the key.
+struct Head {
+  bool active, valid_action;
+  uint4 hdr;
+  int32_t ox, oy, turn;
+  int dir, role;
+  uint32_t cpos;
+  uint64_t kenv;
+};
+
+__device__ __forceinline__ Head head_load(const Params& p, int64_t g, bool active) {
+  Head h;
+  h.active = active;
+  h.hdr = make_uint4(0u, 0u, 0u, 0u);
+  int a = 0;
+  if (active) {
+    h.hdr = p.hdr[g];
+    a = (int)p.actions[g];
+  }
+  h.kenv = env_key(p.seed, (uint64_t)(p.env_base + g));  // overlaps the loads
+  h.ox = xy_x(h.hdr.x);
+  h.oy = xy_y(h.hdr.x);
+  h.turn = (int32_t)h.hdr.y + 1;
+  h.role = (int)misc_role(h.hdr.z);
+  h.dir = DIR_STAY;
+  h.valid_action = a >= 0 && a < p.n_actions;
+  if (h.valid_action) {
+    int dx, dy, nr;
+    decode_action(p, a, dx, dy, nr);
+    h.ox += dx;
+    h.oy += dy;
+    h.dir = dx > 0 ? DIR_RIGHT : dx < 0 ? DIR_LEFT : dy > 0 ? DIR_UP : dy < 0 ? DIR_DOWN : DIR_STAY;
+    if (nr >= 0) h.role = nr;
+  }
+  h.cpos = xy_pack(h.ox, h.oy);
+  return h;
+}
+
+// done (:328-340) from the flags of B1: starve overrides kill, which overrides the old status
+__device__ __forceinline__ bool env_done(const Params& p, const Head& h, bool starved, bool killed) {
+  return starved || killed || misc_status(h.hdr.z) != 0 || h.turn >= p.max_turns;
+}
+
+// spawn draws (spawn_wolves :527-576, wolf iff u < p/2) on ring tiles [r0, r1), r0 % 4 == 0
+__device__ __forceinline__ void ring_part(const Params& p, const Head& h, uint32_t b0, uint32_t b1, int r0, int r1,
+                                          M128& spawn) {
+  const uint32_t ts = make_ts(SITE_SPAWN, 0, h.turn), hk = ts ^ b1;
+  const uint4* ring = reinterpret_cast<const uint4*>(p.tables + p.ring_at);  // uniform: scalar loads
+  for (int r = r0; r < r1; r += 4) {
+    const uint4 o = ring[r >> 2];  // padded to a multiple of 4 entries
+    uint32_t h1[4] = {xy_add(h.cpos, o.x) ^ b0, xy_add(h.cpos, o.y) ^ b0, xy_add(h.cpos, o.z) ^ b0,
+                      xy_add(h.cpos, o.w) ^ b0};
+    fmix32x4(h1);
+    uint32_t hh[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hh[k] = h1[k] ^ hk;
+    fmix32x4(hh);
+    uint32_t hits = 0, tie = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hits |= (hh[k] < p.spawn_th ? 1u : 0u) << k;
+      tie |= (hh[k] == p.spawn_th ? 1u : 0u) << k;
+    }
+    if (tie) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, b0) < p.spawn_tl) hits |= 1u << k;
+    }
+    hits &= r + 4 <= r1 ? 0xFu : (1u << (r1 - r)) - 1u;
+    if (r < 64) spawn.lo |= (uint64_t)hits << r;  // r is a multiple of 4: no straddle
+    else spawn.hi |= (uint64_t)hits << (r - 64);
+  }
+}
+
+// ring split in twelfths (multiples of 4): W2 takes [0, 4/12) before B0, then W1 [4/12, 7/12),
+// W2 [7/12, 9/12), W3 [9/12, 1) between B0 and B1
+__device__ __forceinline__ int ring_cut(const Params& p, int k) { return min(p.R, ((p.R * k / 12) + 3) & ~3); }
+
+// reset draws (generate_bushes, initialize_wolves) of every job for view cells
+// c = c0 + lane, into the jobs' bush / wolf bitmaps
+__device__ __forceinline__ void reset_chunk(const Params& p, const uint32_t* tiles, const uint32_t* jkey, int n_jobs,
+                                            uint32_t c0, int lane, uint32_t* jbm, uint32_t* jwm) {
+  const uint32_t WH = (uint32_t)p.WH;
+  const uint32_t c = c0 + (uint32_t)lane;
+  const uint32_t xy = c < WH ? tiles[c] : 0u;  // ostrich at (0, 0)
+  const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), ts_wolf = make_ts(SITE_SPAWN, 0, 0);
+  for (int j4 = 0; j4 < n_jobs; j4 += 4) {
+    uint32_t kb0[4], kb1[4], h1[4], hb[4], hw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint2 kq = *reinterpret_cast<const uint2*>(&jkey[2 * min(j4 + q, n_jobs - 1)]);
+      kb0[q] = kq.x;
+      kb1[q] = kq.y;
+      h1[q] = xy ^ kq.x;
+    }
+    fmix32x4(h1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      hb[q] = h1[q] ^ ts_bush ^ kb1[q];
+      hw[q] = h1[q] ^ ts_wolf ^ kb1[q];
+    }
+    fmix32x4(hb);
+    fmix32x4(hw);
+    if (c < WH) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (j4 + q >= n_jobs) break;
+        const int jj = j4 + q;
+        if (U_ge(h1[q], hb[q], ts_bush, kb0[q], p.bush_th, p.bush_tl)) atomicOr(&jbm[jj * 4 + (c >> 5)], 1u << (c & 31));
+        if (p.wolves_on && !U_ge(h1[q], hw[q], ts_wolf, kb0[q], p.spawn_th, p.spawn_tl))
+          atomicOr(&jwm[jj * 4 + (c >> 5)], 1u << (c & 31));
+      }
+    }
+  }
+}
+
+// the row or column that scrolled into view (generate_bushes :613-629): its bush bits
+__device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint32_t b0, uint32_t b1) {
+  M128 nb = {0ull, 0ull};
+  if (h.dir != DIR_STAY) {
+    const bool horiz = h.dir == DIR_RIGHT || h.dir == DIR_LEFT;
+    const int n = horiz ? p.H : p.W;
+    const int i0 = h.dir == DIR_LEFT ? p.W - 1 : 0, j0 = h.dir == DIR_DOWN ? p.H - 1 : 0;
+    const uint32_t ts = make_ts(SITE_BUSH, 0, 0), hk = ts ^ b1;
+    for (int c = 0; c < p.SL; c += 4) {
+      uint32_t h1[4], hh[4], cb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = horiz ? i0 : c + k, j = horiz ? c + k : j0;
+        cb[k] = (uint32_t)(i * p.H + j);
+        h1[k] = xy_pack(h.ox - (i - p.cw), h.oy - (j - p.ch)) ^ b0;
+      }
+      fmix32x4(h1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hh[k] = h1[k] ^ hk;
+      fmix32x4(hh);
+      uint32_t hit = 0, tie = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hit |= (hh[k] > p.bush_th ? 1u : 0u) << k;
+        tie |= (hh[k] == p.bush_th ? 1u : 0u) << k;
+      }
+      const uint32_t in = n - c >= 4 ? 0xFu : (n > c ? (1u << (n - c)) - 1u : 0u);
+      if (tie & in) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, b0) >= p.bush_tl) hit |= 1u << k;
+      }
+      hit &= in;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) set_bit_if(nb, cb[k], (hit >> k) & 1u);
+    }
+  }
+  return nb;
+}
+
+struct Lds {
+  uint32_t* tiles;  // [WH] view-cell world offsets (reset draws, initial wolves)
+  uint64_t* thr;    // [max_berries] bush thresholds (W1)
+  uint32_t* stream; // 64 envs x OB bits: bit k = byte k of the group's obs chunk
+  uint32_t* cval;   // [64] generated berries of the ostrich's tile (W1), then flag[0] = 1
+  uint32_t* flag;   // [1] cval ready (zeroed by W0 before B_init)
+  uint4* wolfp;     // [64] wolf grid of S (W2, P0)
+  uint32_t* kill;   // [64] (W2, P0)
+  uint4* bushp;     // [64] bush grid of S (W0, P0)
+  uint32_t* info;   // [64] starved | role << 8 | eaten << 16 | emptied << 24 (W0, P0)
+  uint4* spawn;     // [3][64] ring spawn masks (W1, W2, W3)
+  uint32_t* jbm;    // [job][4] reset bush bitmaps (W3)
+  uint32_t* jwm;    // [job][4] reset wolf cells (W3)
+  uint32_t* jkey;   // [job][2] the new episodes' keys (W3)
+};
+
+__device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
+  Lds s;
+  s.tiles = lds + L.tiles;
+  s.thr = reinterpret_cast<uint64_t*>(lds + L.thr);
+  s.stream = lds + L.stream;
+  s.cval = lds + L.cval;
+  s.flag = lds + L.flag;
+  s.wolfp = reinterpret_cast<uint4*>(lds + L.wolfp);
+  s.kill = lds + L.kill;
+  s.bushp = reinterpret_cast<uint4*>(lds + L.bushp);
+  s.info = lds + L.info;
+  s.spawn = reinterpret_cast<uint4*>(lds + L.spawn);
+  s.jbm = lds + L.jbm;
+  s.jwm = lds + L.jwm;
+  s.jkey = lds + L.jkey;
+  return s;
+}
+
+__device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u; }
+
+// scan eaten-log entries [i0, i0 + 4): the entry on the ostrich's tile, and the emptied
+// tiles in view (absent from S, :506)
+__device__ __forceinline__ void scan_log(const Params& p, const Head& h, const uint32_t* lxy, const uint32_t* lrem,
+                                         int i0, int ne, int& found, int& found_rem, M128& gone) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool in = i0 + k < ne;
+    const uint32_t v = lxy[k];
+    const int r = (int)lrem[k];
+    if (in && v == h.cpos) {
+      found = i0 + k;
+      found_rem = r;
+    }
+    const int ddx = h.ox - xy_x(v), ddy = h.oy - xy_y(v);
+    set_bit_if(gone, (uint32_t)((ddx + p.cw) * p.H + ddy + p.ch), in && r == 0 && abs(ddx) <= p.cw && abs(ddy) <= p.ch);
+  }
+}
+
+// The new episode of a done env (reset :231-248, spawn_ostriches :595-611): state, scalars,
+// initial wolves, and its obs segment (which must be clear) from the job's reset draws.
+template <int SLOTS>
+__device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const Head& h, int64_t g, int j,
+                                            uint32_t ebit, unsigned long long& wolf_of) {
+  const uint32_t WH = (uint32_t)p.WH, ccb = (uint32_t)(p.cw * p.H + p.ch);
+  const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
+  const uint32_t kb0 = (uint32_t)ek2, kb1 = (uint32_t)(ek2 >> 32);
+  const double food2 = p.start_food_random
+                           ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
+                           : p.start_food;
+  const int role2 = p.start_role_random
+                        ? (int)(draw_U(xy_pack(0, 0), make_ts(SITE_START_ROLE, 0, 0), kb0, kb1) >> 52)
+                        : p.start_role;
+  const M128 nbm = m_unpack(*reinterpret_cast<const uint4*>(&s.jbm[4 * j]));
+  const M128 nwm = m_unpack(*reinterpret_cast<const uint4*>(&s.jwm[4 * j]));
+  M128 ost = {0ull, 0ull}, wp = nwm, bp = nbm;
+  m_set(ost, ccb);
+  if (p.restrict_view) {
+    const M128 vm = view_mask_of(p, role2);
+    wp = m_andn(wp, vm);
+    bp = m_andn(bp, vm);
+    ost = m_andn(ost, vm);
+  }
+  stream_or128(s.stream, ebit, wp);
+  stream_or128(s.stream, ebit + WH, bp);
+  stream_or128(s.stream, ebit + 2 * WH, ost);
+  int n = 0;  // initial wolves, one per wolf cell of the view (slot order is irrelevant)
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    uint64_t bits = half ? nwm.hi : nwm.lo;
+    while (bits) {
+      const int b = __ffsll((unsigned long long)bits) - 1;
+      bits &= bits - 1;
+      if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = s.tiles[64 * half + b];
+      else wolf_of += 1;
+    }
+  }
+  p.bushmap[g] = m_word<0>(nbm);
+  if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(nbm);
+  if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(nbm);
+  if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(nbm);
+  p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
+  p.food[g] = food2;
+  p.food_turns[g] = (uint8_t)(int)ceil(food2 * (double)p.turns_empty);
+  p.role[g] = (uint8_t)role2;
+  p.status[g] = 0;
+}
+
+// --------------------------------------------------------------------------- W0: bushes
+template <int SLOTS>
+__device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+  const Lds s = lds_of(lds, L);
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const int64_t g = g0 + lane;
+  const bool active = g < p.B;
+  const uint32_t OB = (uint32_t)p.OB;
+  const uint32_t ccb = (uint32_t)(p.cw * p.H + p.ch);  // the ostrich's cell
+
+  SMALL_STAMP(0);
+  // loads in one round trip (state and the first eaten-log entries, speculatively)
+  double food = 0.0;
+  uint32_t bw0 = 0u, bw1 = 0u, bw2 = 0u, bw3 = 0u;
+  uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
+  const Head h = head_load(p, g, active);
+  if (active) {
+    food = p.food[g];
+    bw0 = p.bushmap[g];
+    if (p.WHW > 1) bw1 = p.bushmap[p.B + g];
+    if (p.WHW > 2) bw2 = p.bushmap[2 * p.B + g];
+    if (p.WHW > 3) bw3 = p.bushmap[3 * p.B + g];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < p.eaten_cap) {
+        lxy[i] = p.eaten_xy[(int64_t)i * p.B + g];
+        lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
+      }
+  }
+  {
+    uint4* z = reinterpret_cast<uint4*>(s.stream);
+    for (uint32_t i = lane; i < L.stream_words / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (lane == 0) s.flag[0] = 0u;
+  lds_barrier();  // B_init: the cval flag is clear
+  int ne = (int)misc_ne(h.hdr.z), ndep = (int)misc_ndep(h.hdr.z);
+  const int status_old = (int)misc_status(h.hdr.z);
+  const int role = h.role;
+  M128 bm = m_make(bw0, bw1, bw2, bw3);  // scroll (generate_bushes keeps the tiles in view, :613-629)
+  if (h.dir == DIR_RIGHT || h.dir == DIR_UP) shl128(bm.lo, bm.hi, h.dir == DIR_RIGHT ? p.H : 1);
+  else if (h.dir == DIR_LEFT || h.dir == DIR_DOWN) shr128(bm.lo, bm.hi, h.dir == DIR_LEFT ? p.H : 1);
+  {
+    const M128 valid = m_make(sreg(p.small_masks[2][0]), sreg(p.small_masks[2][1]), sreg(p.small_masks[2][2]),
+                              sreg(p.small_masks[2][3]));
+    const M128 col0 = m_make(sreg(p.small_masks[0][0]), sreg(p.small_masks[0][1]), sreg(p.small_masks[0][2]),
+                             sreg(p.small_masks[0][3]));
+    const M128 coll = m_make(sreg(p.small_masks[1][0]), sreg(p.small_masks[1][1]), sreg(p.small_masks[1][2]),
+                             sreg(p.small_masks[1][3]));
+    const bool up = h.dir == DIR_UP, down = h.dir == DIR_DOWN;  // the entering column is dropped
+    const M128 drop = {sel64(up, col0.lo, 0ull) | sel64(down, coll.lo, 0ull),
+                       sel64(up, col0.hi, 0ull) | sel64(down, coll.hi, 0ull)};
+    bm = m_andn(m_and(bm, valid), drop);
+  }
+  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
+  const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+  SMALL_STAMP(1);
+  bm = m_or(bm, strip_draws(p, h, b0, b1));
+  SMALL_STAMP(2);
+  // eaten log: the berries left on the ostrich's tile, and emptied tiles that scrolled back
+  // into view (absent from S, :506); the first entries whatever the tile holds (clearing an
+  // emptied tile that is already absent changes nothing), the rest when it can matter
+  int found = -1, found_rem = 0;
+  {
+    M128 gone = {0ull, 0ull};
+    scan_log(p, h, lxy, lrem, 0, ne, found, found_rem, gone);
+    bm = m_andn(bm, gone);
+  }
+  bool center_bush = m_test(bm, ccb);
+  if (ne > 4 && (center_bush || (ndep > 0 && h.dir != DIR_STAY))) {
+    for (int i0 = 4; i0 < ne; i0 += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (i0 + k < ne) {
+          lxy[k] = p.eaten_xy[(int64_t)(i0 + k) * p.B + g];
+          lrem[k] = p.eaten_rem[(int64_t)(i0 + k) * p.B + g];
+        }
+      M128 gone = {0ull, 0ull};
+      scan_log(p, h, lxy, lrem, i0, ne, found, found_rem, gone);
+      bm = m_andn(bm, gone);
+    }
+    center_bush = m_test(bm, ccb);
+  }
+  SMALL_STAMP(7);
+  s.bushp[lane] = m_pack(bm);  // bush grid of S (pre-eat)
+  int rem = found_rem;         // berries left: the log, else the generated value (W1)
+  if (found < 0) {
+    rem = 0;
+    if (center_bush) {
+      // W1 publishes the values right after B_init; the bound only guards against a hang
+      for (int spin = 0; spin < (1 << 20); ++spin) {
+        if (__hip_atomic_load(s.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      rem = (int)s.cval[lane];
+    }
+  }
+  SMALL_STAMP(8);
+  double reward = 0.0;
+  unsigned long long eaten_of = 0;
+  if (rem > 0 && status_old == 0 && (role == 1 || p.lookout_only)) {  // eat (:299-313), stale status
+    food = food + p.fill;
+    food = food < 0.0 ? 0.0 : (food > 1.0 ? 1.0 : food);
+    reward += p.r_eat;
+    bool logged = true;
+    if (found >= 0) {
+      p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
+    } else if (ne < p.eaten_cap) {
+      p.eaten_xy[(int64_t)ne * p.B + g] = h.cpos;
+      p.eaten_rem[(int64_t)ne * p.B + g] = (uint8_t)(rem - 1);
+      ne += 1;
+    } else {
+      eaten_of += 1;
+      logged = false;
+    }
+    if (rem == 1) {  // emptied: gone from the cached view from the next step on
+      m_clear(bm, ccb);
+      if (logged) ndep += 1;
+    }
+  }
+  food = food - p.hunger;  // :316-322
+  const bool starved = food <= 0.0;
+  if (starved) food = 0.0;
+  s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
+  SMALL_STAMP(3);
+  lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
+
+  // status (starve overrides kill), reward/done (:328-340), scalars, bushes and food
+  const bool killed = s.kill[lane] != 0u;
+  const int status = starved ? 1 : killed ? 2 : status_old;
+  const bool done = env_done(p, h, starved, killed);
+  {
+    const double r_finish = sreg(p.r_finish), r_turn = sreg(p.r_turn);
+    const double r_starve = sreg(p.r_starve), r_killed = sreg(p.r_killed);
+    reward += sel_f64(status == 0, sel_f64(done, r_finish, r_turn), sel_f64(status == 1, r_starve, r_killed));
+  }
+  const bool job = active && done && p.autoreset;
+  if (active) {
+    const int ft = (int)ceil(food * (double)p.turns_empty);  // :450-452
+    p.reward[g] = (float)reward;
+    p.done[g] = done ? 1 : 0;
+    // a done env's own scalars go to the terminal side buffer (pointers chosen by masks: an
+    // if/else of the two stores is merged into a scratch-indexed pointer pair)
+    uint8_t* fts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_food_turns, (uint64_t)p.food_turns));
+    uint8_t* rls = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_role, (uint64_t)p.role));
+    uint8_t* sts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_status, (uint64_t)p.status));
+    if (!job || p.t_planes) {
+      fts[g] = (uint8_t)ft;
+      rls[g] = (uint8_t)role;
+      sts[g] = (uint8_t)status;
+    }
+    if (!job) {
+      p.bushmap[g] = m_word<0>(bm);
+      if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(bm);
+      if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(bm);
+      if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(bm);
+      p.food[g] = food;
+    }
+  }
+  if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
+  if (active && !h.valid_action) atomicAdd(&p.counters[2], 1ull);
+  const unsigned long long jm = __ballot(job);
+  if (lane == 0 && jm) p.block_resets[blockIdx.x] += (unsigned long long)__popcll(jm);
+  SMALL_STAMP(4);
+  lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
+  if (p.t_planes) {
+    // terminal obs: the step's own obs of every done env (bytes); then its new episode
+    unsigned long long wolf_of = 0;
+    if (jm) {
+      uint8_t* tout = p.t_planes + (size_t)g0 * OB;
+      for (unsigned long long jj = jm; jj; jj &= jj - 1) {
+        const uint32_t ee = (uint32_t)(__ffsll(jj) - 1);
+        for (uint32_t k = lane; k < OB; k += 64) {
+          const uint32_t bit = ee * OB + k;
+          tout[bit] = (uint8_t)((s.stream[bit >> 5] >> (bit & 31)) & 1u);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (job) {
+        const uint32_t ebit = (uint32_t)lane * OB;
+        stream_clear(s.stream, ebit, OB);
+        new_episode<SLOTS>(p, s, h, g, __popcll(jm & ((1ull << lane) - 1ull)), ebit, wolf_of);
+      }
+    }
+    if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+    lds_barrier();  // B3
+  }
+  SMALL_STAMP(5);
+}
+
+// --------------------------------------------------------------------------- W1: draws
+__device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+  const Lds s = lds_of(lds, L);
+  const int64_t g = (int64_t)blockIdx.x * 64 + lane;
+  const uint32_t OB = (uint32_t)p.OB, WH = (uint32_t)p.WH;
+  SMALL_STAMP(10);
+  const Head h = head_load(p, g, g < p.B);
+  for (int k = lane; k < p.max_berries; k += 64) s.thr[k] = p.thresholds[k];
+  lds_barrier();  // B_init
+  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
+  const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+  // the generated berries of the ostrich's tile (:631-635), for W0
+  s.cval[lane] = (uint32_t)bush_value(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(s.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  SMALL_STAMP(11);
+  // ring part A
+  M128 spawn = {0ull, 0ull};
+  if (p.wolves_on) ring_part(p, h, b0, b1, 0, ring_cut(p, 4), spawn);
+  s.spawn[lane] = m_pack(spawn);
+  SMALL_STAMP(12);
+  lds_barrier();  // B1
+  // render S (:393-444) for the continuing envs (and the done ones when their terminal obs
+  // is asked for)
+  const uint32_t info = s.info[lane];
+  const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), s.kill[lane] != 0u);
+  if (h.active && (!job || p.t_planes)) {
+    const uint32_t ebit = (uint32_t)lane * OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
+    M128 ost = {0ull, 0ull};
+    m_set(ost, ccb);
+    M128 wp = m_unpack(s.wolfp[lane]), bp = m_unpack(s.bushp[lane]);
+    if (p.restrict_view) {  // mask_grid (:344-357) by the fresh role
+      const M128 vm = view_mask_of(p, (int)((info >> 8) & 0xFFu));
+      wp = m_andn(wp, vm);
+      bp = m_andn(bp, vm);
+      ost = m_andn(ost, vm);
+    }
+    stream_or128(s.stream, ebit, wp);
+    stream_or128(s.stream, ebit + WH, bp);
+    stream_or128(s.stream, ebit + 2 * WH, ost);
+  }
+  SMALL_STAMP(13);
+  lds_barrier();  // B2
+  if (p.t_planes) lds_barrier();  // B3
+  SMALL_STAMP(14);
+}
+
+// --------------------------------------------------------------------------- W2: wolves
+template <int SLOTS>
+__device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+  const Lds s = lds_of(lds, L);
+  const int64_t g = (int64_t)blockIdx.x * 64 + lane;
+  const bool active = g < p.B;
+  SMALL_STAMP(16);
+  uint32_t wr[SLOTS];
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // slots 0..3 speculatively
+  }
+  const Head h = head_load(p, g, active);
+  lds_barrier();  // B_init
+  const int nw = (int)misc_nw(h.hdr.z);
+#pragma unroll
+  for (int k = 4; k < SLOTS; ++k)
+    if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
+  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
+  const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+  uint32_t live = nw >= 32 ? ~0u : ((1u << nw) - 1u);
+
+  // despawn (:262-264): one draw per wolf, keyed by its tile and its occurrence index among
+  // the co-located wolves before it; groups of 4 slots, skipped when no lane has a wolf there
+  {
+    uint32_t keep = 0;
+#pragma unroll
+    for (int g4 = 0; g4 < SLOTS; g4 += 4) {
+      const uint32_t live4 = (live >> g4) & 0xFu;
+      if (!live4) continue;
+      uint32_t h1[4], hh[4], ts[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = g4 + q;
+        uint32_t occ = 0;
+#pragma unroll
+        for (int t = 0; t < k; ++t) occ += (((live >> t) & 1u) && wr[t] == wr[k]) ? 1u : 0u;
+        ts[q] = make_ts(SITE_DESPAWN, occ, h.turn);
+        h1[q] = wr[k] ^ b0;
+      }
+      fmix32x4(h1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hh[q] = h1[q] ^ ts[q] ^ b1;
+      fmix32x4(hh);
+      uint32_t kp = 0, tie = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kp |= (hh[q] > p.keep_th ? 1u : 0u) << q;
+        tie |= (hh[q] == p.keep_th ? 1u : 0u) << q;
+      }
+      if (tie & live4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (((tie >> q) & 1u) && draw_lo21(h1[q], ts[q], b0) >= p.keep_tl) kp |= 1u << q;
+      }
+      keep |= (kp & live4) << g4;
+    }
+    live = keep;
+  }
+  // pursuit (:267-286): one axis step toward the ostrich, ties along x; grid of S; kill
+  M128 wolfp = {0ull, 0ull};
+  bool kill = false;
+#pragma unroll
+  for (int g4 = 0; g4 < SLOTS; g4 += 4) {
+    if (!((live >> g4) & 0xFu)) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = g4 + q;
+      const bool on = (live >> k) & 1u;
+      int wx = xy_x(wr[k]), wy = xy_y(wr[k]);
+      if (p.wolves_can_move) {
+        const int ddx = h.ox - wx, ddy = h.oy - wy;
+        const bool alongx = abs(ddx) >= abs(ddy);
+        wx += alongx ? sgn(ddx) : 0;
+        wy += alongx ? 0 : sgn(ddy);
+        wr[k] = xy_pack(wx, wy);
+      }
+      const int ddx = h.ox - wx, ddy = h.oy - wy;
+      set_bit_if(wolfp, (uint32_t)((ddx + p.cw) * p.H + ddy + p.ch), on && abs(ddx) <= p.cw && abs(ddy) <= p.ch);
+      kill |= on && ddx == 0 && ddy == 0;
+    }
+  }
+  kill = kill && !p.god_mode;  // :291-297
+  s.wolfp[lane] = m_pack(wolfp);
+  s.kill[lane] = kill ? 1u : 0u;
+  SMALL_STAMP(17);
+  // ring part B
+  M128 spawn = {0ull, 0ull};
+  if (p.wolves_on) ring_part(p, h, b0, b1, ring_cut(p, 4), ring_cut(p, 7), spawn);
+  s.spawn[64 + lane] = m_pack(spawn);
+  SMALL_STAMP(18);
+  lds_barrier();  // B1: every ring part, the starve flags and the bushes' counts are in
+
+  // spawn_wolves (:325-326): new wolves into free slots (outside the view, not in S)
+  unsigned long long wolf_of = 0;
+  spawn = m_or(m_or(m_unpack(s.spawn[lane]), m_unpack(s.spawn[64 + lane])), m_unpack(s.spawn[128 + lane]));
+  if (active && (spawn.lo | spawn.hi)) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      uint64_t bits = half ? spawn.hi : spawn.lo;
+      while (bits) {
+        const int b = __ffsll((unsigned long long)bits) - 1;
+        bits &= bits - 1;
+        const uint32_t w = xy_add(h.cpos, p.tables[p.ring_at + 64 * half + b]);
+        bool placed = false;
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k)
+          if (!placed && !((live >> k) & 1u)) { wr[k] = w; live |= 1u << k; placed = true; }
+        if (!placed) wolf_of += 1;
+      }
+    }
+  }
+  // the next state of a continuing env: wolf slots and header (a done env's come from its
+  // new episode)
+  const uint32_t info = s.info[lane];
+  const bool starved = info_starved(info);
+  const bool job = active && p.autoreset && env_done(p, h, starved, kill);
+  if (active && !job) {
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k)
+      if ((live >> k) & 1u) p.wolves[(int64_t)(n++) * p.B + g] = wr[k];
+    const uint32_t status = starved ? 1u : kill ? 2u : misc_status(h.hdr.z);
+    p.hdr[g] = make_uint4(h.cpos, (uint32_t)h.turn,
+                          misc_pack((info >> 8) & 0xFFu, status, (uint32_t)n, (info >> 16) & 0xFFu, info >> 24),
+                          h.hdr.w);
+  }
+  if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+  SMALL_STAMP(19);
+  lds_barrier();  // B2
+  if (p.t_planes) lds_barrier();  // B3
+  SMALL_STAMP(20);
+}
+
+// --------------------------------------------------------------------------- W3: ring
+template <int SLOTS>
+__device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+  const Lds s = lds_of(lds, L);
+  const int64_t g = (int64_t)blockIdx.x * 64 + lane;
+  SMALL_STAMP(22);
+  const Head h = head_load(p, g, g < p.B);
+  for (int c = lane; c < p.WH; c += 64) s.tiles[c] = p.tables[c];
+  {  // zero the reset tables (jbm, jwm: [64][4] each, contiguous)
+    uint4* z = reinterpret_cast<uint4*>(s.jbm);
+    for (int i = lane; i < 2 * 64; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  lds_barrier();  // B_init
+  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
+  const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+  // ring part C
+  M128 spawn = {0ull, 0ull};
+  if (p.wolves_on) ring_part(p, h, b0, b1, ring_cut(p, 7), p.R, spawn);
+  s.spawn[128 + lane] = m_pack(spawn);
+  SMALL_STAMP(23);
+  lds_barrier();  // B1
+  // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
+  // (unless the terminal obs is asked for: W0 after B2) the new episodes themselves
+  const bool job = h.active && p.autoreset && env_done(p, h, info_starved(s.info[lane]), s.kill[lane] != 0u);
+  const unsigned long long jm = __ballot(job);
+  if (jm) {
+    const int j = __popcll(jm & ((1ull << lane) - 1ull));
+    if (job) {
+      const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
+      *reinterpret_cast<uint2*>(&s.jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
+    }
+    const int n_jobs = __popcll(jm);
+    for (uint32_t c0 = 0; c0 < (uint32_t)p.WH; c0 += 64)
+      reset_chunk(p, s.tiles, s.jkey, n_jobs, c0, lane, s.jbm, s.jwm);
+    if (!p.t_planes) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      unsigned long long wolf_of = 0;
+      if (job) new_episode<SLOTS>(p, s, h, g, j, (uint32_t)lane * (uint32_t)p.OB, wolf_of);
+      if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+    }
+  }
+  SMALL_STAMP(25);
+  lds_barrier();  // B2
+  if (p.t_planes) lds_barrier();  // B3
+  SMALL_STAMP(26);
+}
+
+// --------------------------------------------------------------------------- obs stores
+// expand the 64-env bit-stream and store it with 16-byte stores, all 256 threads
+__device__ __forceinline__ void store_obs(const Params& p, const uint32_t* stream, int tid) {
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const uint32_t OB = (uint32_t)p.OB;
+  const uint32_t limit = (uint32_t)min((int64_t)64, p.B - g0) * OB;
+  uint8_t* out = p.planes + (size_t)g0 * OB;
+  const uint32_t sw = (limit + 31u) >> 5;
+  for (uint32_t d = tid; d < sw; d += 256) {
+    const uint32_t bo = d << 5;
+    const uint32_t v = stream[d];
+    if (bo + 32u <= limit) {
+      uint4 q0, q1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) (&q0.x)[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) (&q1.x)[k] = (((v >> (16 + 4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+      *reinterpret_cast<uint4*>(out + bo) = q0;
+      *reinterpret_cast<uint4*>(out + bo + 16) = q1;
+    } else {
+      for (uint32_t k = 0; bo + k < limit; ++k) out[bo + k] = (uint8_t)((v >> k) & 1u);
+    }
+  }
+#ifdef WAB_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((tid & 63) == 0 && p.stamps) {
+    const int slot[4] = {6, 15, 21, 27};
+    p.stamps[(size_t)blockIdx.x * 32 + slot[tid >> 6]] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+}
+
+}  // namespace
+
+template <int SLOTS>
+__global__ __launch_bounds__(256) void wab_step_small(Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const SmallLayout L = small_layout(p);
+  if ((int64_t)blockIdx.x * 64 >= p.B) return;  // (uniform over the workgroup)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave == 0) bushes_wave<SLOTS>(p, L, lds, lane);
+  else if (wave == 1) draws_wave(p, L, lds, lane);
+  else if (wave == 2) wolves_wave<SLOTS>(p, L, lds, lane);
+  else ring_wave<SLOTS>(p, L, lds, lane);
+  store_obs(p, lds + L.stream, threadIdx.x);
+}
+
+template __global__ void wab_step_small<8>(Params);
+template __global__ void wab_step_small<16>(Params);
+template __global__ void wab_step_small<32>(Params);
+
+}  // namespace wab
