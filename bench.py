@@ -26,9 +26,10 @@ METRIC = "env-steps/sec (whole node) at batch=65536; obs bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 CONFIGS = {
-    # name: (game options, plane_stride, description)
-    "default": ({}, 0, "batch=65536 envs x default options (11x11 viewport), random policy, autoreset"),
-    "wide31": ({"width": 31, "height": 31}, 32,
+    # name: (game options, plane_stride, wolf slots, description)
+    "default": ({}, 0, 8, "batch=65536 envs x default options (11x11 viewport), random policy, autoreset"),
+    # 16 wolf slots: with 8, a 961-cell reset view overflows a few times per million resets
+    "wide31": ({"width": 31, "height": 31}, 32, 16,
                "batch=65536 envs x 31x31 viewport in 32x32 planes (C3), random policy, autoreset"),
 }
 
@@ -99,11 +100,12 @@ def main():
     from wab_gym_amd import _lib
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
 
-    opts, stride, desc = CONFIGS[args.config]
+    opts, stride, slots, desc = CONFIGS[args.config]
     B, K, W = args.batch, args.steps, args.warmup
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
                                     env_id_base=env_id_base(rank, B),
-                                    autoreset=True, validate_actions=False, plane_stride=stride)
+                                    autoreset=True, validate_actions=False, plane_stride=stride,
+                                    wolf_slots=slots)
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)

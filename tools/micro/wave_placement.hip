@@ -20,10 +20,10 @@ __global__ void probe(uint32_t* out, int iters) {
 }
 
 int main() {
-  const int total_waves = 1024 * 2;
+  const int total_waves = 1024 * 4;
   uint32_t* d;
   (void)hipMalloc(&d, total_waves * 8);
-  for (int wpg : {1, 2, 4}) {
+  for (int wpg : {4}) {
     const int blocks = total_waves / wpg;
     (void)hipMemset(d, 0, total_waves * 8);
     probe<<<blocks, 64 * wpg>>>(d, 20000);

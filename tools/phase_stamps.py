@@ -34,10 +34,10 @@ def main():
     from wab_gym_amd import _lib
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
 
-    opts, stride, _ = bench.CONFIGS[args.config]
+    opts, stride, slots, _ = bench.CONFIGS[args.config]
     B = args.batch
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, device="cuda:0", validate_actions=False,
-                                    plane_stride=stride)
+                                    plane_stride=stride, wolf_slots=slots)
     L = _lib.load()
     L.wab_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     nb = (B + 63) // 64
@@ -108,6 +108,7 @@ def small_report(env, st, g, steps):
                                                    "obs stores"])}
     acc = {k: [] for k in waves}
     spans, ends = [], []
+    by_xcd, slow_w0, fast_w0, start_off = [], [], [], []
     for t in range(steps):
         st.zero_()
         env.step(torch.randint(0, env.n_actions, (B,), device="cuda:0", generator=g))
@@ -121,6 +122,14 @@ def small_report(env, st, g, steps):
         end = s[:, [6, 15, 21, 27]].max(axis=1)
         spans.append(end.max() - t0)
         ends.append(np.percentile(end - t0, [0, 50, 100]))
+        xcd = np.arange(len(end)) % 8
+        by_xcd.append([(end - t0)[xcd == x].mean() for x in range(8)])
+        order = np.argsort(end)
+        cols0 = waves["W0 bushes"][0]
+        d0 = np.diff(s[:, cols0], axis=1)
+        slow_w0.append(d0[order[-len(order) // 20:]].mean(axis=0))
+        fast_w0.append(d0[order[: len(order) // 4]].mean(axis=0))
+        start_off.append(((s[:, 0] - t0)[order[-len(order) // 20:]].mean(), (s[:, 0] - t0)[order[: len(order) // 4]].mean()))
     for k, (cols, names) in waves.items():
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s:" % k)
@@ -128,6 +137,10 @@ def small_report(env, st, g, steps):
             print("  %-28s %7.2f us" % (n, v))
     print("%-24s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
     print("workgroup end times p0/p50/max (us):", np.round(np.mean(ends, axis=0) * 10 / 1000, 2))
+    print("mean end time by blockIdx %% 8 (us):", np.round(np.mean(by_xcd, axis=0) * 10 / 1000, 2))
+    print("W0 phases, slowest 5%% of workgroups (us):", np.round(np.mean(slow_w0, axis=0) * 10 / 1000, 2))
+    print("W0 phases, fastest 25%% of workgroups (us):", np.round(np.mean(fast_w0, axis=0) * 10 / 1000, 2))
+    print("W0 start offset slowest 5%% / fastest 25%% (us):", np.round(np.mean(start_off, axis=0) * 10 / 1000, 2))
 
 
 if __name__ == "__main__":

@@ -139,10 +139,10 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.kill = o; o += 64u;
   L.bushp = o; o += 64u * 4u;
   L.info = o; o += 64u;
-  L.spawn = o; o += 3u * 64u * 4u;
+  L.spawn = o; o += 4u * 64u * 4u;
   L.jbm = o; o += 64u * 4u;
   L.jwm = o; o += 64u * 4u;  // (directly after jbm: zeroed together)
-  L.jkey = o; o += 2u * 64u;
+  L.jkey = o; o += 2u * 2u * 64u;
   L.total = o;
   return L;
 }

@@ -609,13 +609,15 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       else v = sB[d];
       const uint32_t write_mask = (MODE == MODE_STEP) ? ~0u : dm;
       if (write_mask == ~0u && bo + 32u <= limit) {
-        uint4 q0, q1;
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 q0, q1;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) (&q0.x)[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        for (int k = 0; k < 4; ++k) q0[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) (&q1.x)[k] = (((v >> (16 + 4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-        *reinterpret_cast<uint4*>(out + bo) = q0;
-        *reinterpret_cast<uint4*>(out + bo + 16) = q1;
+        for (int k = 0; k < 4; ++k) q1[k] = (((v >> (16 + 4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        // streamed out, never re-read by the kernel: non-temporal (no L2 allocation)
+        __builtin_nontemporal_store(q0, reinterpret_cast<u32x4*>(out + bo));
+        __builtin_nontemporal_store(q1, reinterpret_cast<u32x4*>(out + bo + 16));
       } else if (write_mask) {
         for (uint32_t k = 0; k < 32u && bo + k < limit; ++k)
           if ((write_mask >> k) & 1u) out[bo + k] = (uint8_t)((v >> k) & 1u);

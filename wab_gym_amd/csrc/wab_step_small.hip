@@ -131,8 +131,8 @@ __device__ __forceinline__ void ring_part(const Params& p, const Head& h, uint32
   }
 }
 
-// ring split in twelfths (multiples of 4): W2 takes [0, 4/12) before B0, then W1 [4/12, 7/12),
-// W2 [7/12, 9/12), W3 [9/12, 1) between B0 and B1
+// the spawn ring split in twelfths (multiples of 4), balanced against each wave's other work
+// before B1: W0 [0, 2/12), W1 [2/12, 4/12), W2 [4/12, 7/12), W3 [7/12, 1)
 __device__ __forceinline__ int ring_cut(const Params& p, int k) { return min(p.R, ((p.R * k / 12) + 3) & ~3); }
 
 // reset draws (generate_bushes, initialize_wolves) of every job for view cells
@@ -218,15 +218,15 @@ struct Lds {
   uint64_t* thr;    // [max_berries] bush thresholds (W1)
   uint32_t* stream; // 64 envs x OB bits: bit k = byte k of the group's obs chunk
   uint32_t* cval;   // [64] generated berries of the ostrich's tile (W1), then flag[0] = 1
-  uint32_t* flag;   // [1] cval ready (zeroed by W0 before B_init)
+  uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done; zeroed by W0 before B_init
   uint4* wolfp;     // [64] wolf grid of S (W2, P0)
   uint32_t* kill;   // [64] (W2, P0)
   uint4* bushp;     // [64] bush grid of S (W0, P0)
   uint32_t* info;   // [64] starved | role << 8 | eaten << 16 | emptied << 24 (W0, P0)
-  uint4* spawn;     // [3][64] ring spawn masks (W1, W2, W3)
-  uint32_t* jbm;    // [job][4] reset bush bitmaps (W3)
-  uint32_t* jwm;    // [job][4] reset wolf cells (W3)
-  uint32_t* jkey;   // [job][2] the new episodes' keys (W3)
+  uint4* spawn;     // [4][64] ring spawn masks (W1, W2, W3, W0)
+  uint32_t* jbm;    // [job][4] reset bush bitmaps (W1, W3)
+  uint32_t* jwm;    // [job][4] reset wolf cells (W1, W3)
+  uint32_t* jkey;   // [2][job][2] the new episodes' keys: W1's copy, W3's copy
 };
 
 __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
@@ -349,8 +349,11 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
     uint4* z = reinterpret_cast<uint4*>(s.stream);
     for (uint32_t i = lane; i < L.stream_words / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
-  if (lane == 0) s.flag[0] = 0u;
-  lds_barrier();  // B_init: the cval flag is clear
+  if (lane == 0) {
+    s.flag[0] = 0u;
+    s.flag[1] = 0u;
+  }
+  lds_barrier();  // B_init: the hand-off flags are clear
   int ne = (int)misc_ne(h.hdr.z), ndep = (int)misc_ndep(h.hdr.z);
   const int status_old = (int)misc_status(h.hdr.z);
   const int role = h.role;
@@ -439,6 +442,11 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   const bool starved = food <= 0.0;
   if (starved) food = 0.0;
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
+  {  // spawn ring part W0 (the helpers' parts are longer: they start it earlier)
+    M128 spawn = {0ull, 0ull};
+    if (p.wolves_on) ring_part(p, h, b0, b1, 0, ring_cut(p, 2), spawn);
+    s.spawn[192 + lane] = m_pack(spawn);
+  }
   SMALL_STAMP(3);
   lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
 
@@ -454,8 +462,8 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   const bool job = active && done && p.autoreset;
   if (active) {
     const int ft = (int)ceil(food * (double)p.turns_empty);  // :450-452
-    p.reward[g] = (float)reward;
-    p.done[g] = done ? 1 : 0;
+    __builtin_nontemporal_store((float)reward, p.reward + g);
+    __builtin_nontemporal_store((uint8_t)(done ? 1 : 0), p.done + g);
     // a done env's own scalars go to the terminal side buffer (pointers chosen by masks: an
     // if/else of the two stores is merged into a scratch-indexed pointer pair)
     uint8_t* fts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_food_turns, (uint64_t)p.food_turns));
@@ -511,6 +519,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   const uint32_t OB = (uint32_t)p.OB, WH = (uint32_t)p.WH;
   SMALL_STAMP(10);
+  __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
   const Head h = head_load(p, g, g < p.B);
   for (int k = lane; k < p.max_berries; k += 64) s.thr[k] = p.thresholds[k];
   lds_barrier();  // B_init
@@ -520,10 +529,11 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   s.cval[lane] = (uint32_t)bush_value(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1));
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_store(s.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_s_setprio(0);
   SMALL_STAMP(11);
-  // ring part A
+  // spawn ring part W1
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part(p, h, b0, b1, 0, ring_cut(p, 4), spawn);
+  if (p.wolves_on) ring_part(p, h, b0, b1, ring_cut(p, 2), ring_cut(p, 4), spawn);
   s.spawn[lane] = m_pack(spawn);
   SMALL_STAMP(12);
   lds_barrier();  // B1
@@ -545,6 +555,19 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
     stream_or128(s.stream, ebit, wp);
     stream_or128(s.stream, ebit + WH, bp);
     stream_or128(s.stream, ebit + 2 * WH, ost);
+  }
+  // the reset draws of the done envs for view cells [0, 64); W3 draws the rest and waits for
+  // flag[1] before it builds the new episodes
+  const unsigned long long jm = __ballot(job);
+  if (jm) {
+    if (job) {
+      const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
+      const int j = __popcll(jm & ((1ull << lane) - 1ull));
+      *reinterpret_cast<uint2*>(&s.jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
+    }
+    reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm, s.jwm);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&s.flag[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   SMALL_STAMP(13);
   lds_barrier();  // B2
@@ -649,7 +672,8 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
 
   // spawn_wolves (:325-326): new wolves into free slots (outside the view, not in S)
   unsigned long long wolf_of = 0;
-  spawn = m_or(m_or(m_unpack(s.spawn[lane]), m_unpack(s.spawn[64 + lane])), m_unpack(s.spawn[128 + lane]));
+  spawn = m_or(m_or(m_unpack(s.spawn[lane]), m_unpack(s.spawn[64 + lane])),
+               m_or(m_unpack(s.spawn[128 + lane]), m_unpack(s.spawn[192 + lane])));
   if (active && (spawn.lo | spawn.hi)) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -715,14 +739,19 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
   const unsigned long long jm = __ballot(job);
   if (jm) {
     const int j = __popcll(jm & ((1ull << lane) - 1ull));
+    uint32_t* jkey = s.jkey + 2 * 64;  // this wave's copy of the keys
     if (job) {
       const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
-      *reinterpret_cast<uint2*>(&s.jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
+      *reinterpret_cast<uint2*>(&jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
     }
     const int n_jobs = __popcll(jm);
-    for (uint32_t c0 = 0; c0 < (uint32_t)p.WH; c0 += 64)
-      reset_chunk(p, s.tiles, s.jkey, n_jobs, c0, lane, s.jbm, s.jwm);
+    for (uint32_t c0 = 64; c0 < (uint32_t)p.WH; c0 += 64)  // cells [0, 64): W1
+      reset_chunk(p, s.tiles, jkey, n_jobs, c0, lane, s.jbm, s.jwm);
     if (!p.t_planes) {
+      for (int spin = 0; spin < (1 << 20); ++spin) {  // W1's part of the draws (bounded wait)
+        if (__hip_atomic_load(&s.flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       unsigned long long wolf_of = 0;
       if (job) new_episode<SLOTS>(p, s, h, g, j, (uint32_t)lane * (uint32_t)p.OB, wolf_of);
@@ -742,22 +771,19 @@ __device__ __forceinline__ void store_obs(const Params& p, const uint32_t* strea
   const uint32_t OB = (uint32_t)p.OB;
   const uint32_t limit = (uint32_t)min((int64_t)64, p.B - g0) * OB;
   uint8_t* out = p.planes + (size_t)g0 * OB;
-  const uint32_t sw = (limit + 31u) >> 5;
-  for (uint32_t d = tid; d < sw; d += 256) {
-    const uint32_t bo = d << 5;
-    const uint32_t v = stream[d];
-    if (bo + 32u <= limit) {
-      uint4 q0, q1;
+  // one 16-bit unit of the stream -> 16 bytes: each wave-instruction stores 1 KiB contiguous
+  const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stream);
+  const uint32_t full = limit >> 4;
+  for (uint32_t u = tid; u < full; u += 256) {
+    const uint32_t v = s16[u];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 q;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) (&q0.x)[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) (&q1.x)[k] = (((v >> (16 + 4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-      *reinterpret_cast<uint4*>(out + bo) = q0;
-      *reinterpret_cast<uint4*>(out + bo + 16) = q1;
-    } else {
-      for (uint32_t k = 0; bo + k < limit; ++k) out[bo + k] = (uint8_t)((v >> k) & 1u);
-    }
+    for (int k = 0; k < 4; ++k) q[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
   }
+  for (uint32_t b = (full << 4) + tid; b < limit; b += 256)  // a partial last group
+    out[b] = (uint8_t)((stream[b >> 5] >> (b & 31)) & 1u);
 #ifdef WAB_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if ((tid & 63) == 0 && p.stamps) {
@@ -775,8 +801,15 @@ __global__ __launch_bounds__(256) void wab_step_small(Params p) {
   const SmallLayout L = small_layout(p);
   if ((int64_t)blockIdx.x * 64 >= p.B) return;  // (uniform over the workgroup)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave == 0) bushes_wave<SLOTS>(p, L, lds, lane);
-  else if (wave == 1) draws_wave(p, L, lds, lane);
+  if (wave == 0) {
+    // the bushes wave carries the longest chain and shares its SIMD with three helper waves
+    // of other groups: let the arbiter issue its instructions first
+    __builtin_amdgcn_s_setprio(3);
+    bushes_wave<SLOTS>(p, L, lds, lane);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  else if (wave == 1)
+    draws_wave(p, L, lds, lane);
   else if (wave == 2) wolves_wave<SLOTS>(p, L, lds, lane);
   else ring_wave<SLOTS>(p, L, lds, lane);
   store_obs(p, lds + L.stream, threadIdx.x);
