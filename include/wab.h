@@ -22,6 +22,8 @@
  *                            with pre-chosen actions (T fused steps)
  *   wab_destroy           <- (gym.Env.close; nothing to free in the reference)
  *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
+ *   wab_featurize_superbasic <- SuperBasicObservationWrapper.observation wab_env.py:900-927
+ *   wab_render            <- WolvesAndBushesEnv.render (rgb_array)   wab_env.py:468-502
  *                            + gym.spaces.flatten                    actor_critic.py:188
  *   wab_discounted_returns<- finish_episode's return loop             actor_critic.py:139-143
  */
@@ -185,6 +187,17 @@ int wab_feature_dim(const wab_handle* h);
  * options as _get_obs does (wab_env.py:360-368). */
 int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
                   void* stream);
+
+/* SuperBasicObservationWrapper.observation (wab_env.py:900-927) + gym flatten: the nearest
+ * bush of the bush grid (4 x Discrete(max_distance)), food, role, status -> one-hot float32
+ * [B][wab_superbasic_dim(h)] (90 for the defaults).  features must be 16-byte aligned. */
+int wab_superbasic_dim(const wab_handle* h);
+int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features, void* stream);
+
+/* WolvesAndBushesEnv.render(mode="rgb_array", scale, draw_health=False) (wab_env.py:468-502)
+ * of an observation this handle produced: rgb [B][W*scale][H*scale][3] u8 device pointer.
+ * The food-count text overlay of draw_health=True (PIL font) is not drawn. */
+int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, void* stream);
 
 /* Discounted returns of actor_critic.finish_episode (actor_critic.py:139-143) over a
  * [T][B] rollout: R_t = r_t + gamma * R_{t+1}, restarted after every done_t, R_T =

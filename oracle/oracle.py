@@ -50,6 +50,9 @@ def lib():
                                   ctypes.c_int64, ctypes.c_uint32]
         L.wabo_feature_dim.argtypes = [ctypes.c_int] * 3
         L.wabo_featurize.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 6
+        L.wabo_superbasic_dim.argtypes = [ctypes.c_int] * 3
+        L.wabo_render.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 5 + [P] * 4
+        L.wabo_featurize_superbasic.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 5
         L.wabo_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_double, P, P]
         _lib = L
     return _lib
@@ -137,6 +140,32 @@ def featurize(planes, food_turns, role, status, view_mask, W, H, turns_empty=40)
     arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in (food_turns, role, status, view_mask)]
     lib().wabo_featurize(B, W, H, S, turns_empty, _p(planes), _p(arrs[0]), _p(arrs[1]), _p(arrs[2]),
                          _p(arrs[3]), _p(out))
+    return out
+
+
+def superbasic_dim(W=11, H=11, turns_empty=40):
+    return int(lib().wabo_superbasic_dim(W, H, turns_empty))
+
+
+def featurize_superbasic(planes, food_turns, role, status, W, H, turns_empty=40):
+    """SuperBasicObservationWrapper + flatten: planes [B,3,W,S] u8, scalars [B] u8 -> f32 [B, F]."""
+    planes = np.ascontiguousarray(planes, dtype=np.uint8)
+    B, S = planes.shape[0], planes.shape[3]
+    out = np.zeros((B, superbasic_dim(W, H, turns_empty)), np.float32)
+    arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in (food_turns, role, status)]
+    lib().wabo_featurize_superbasic(B, W, H, S, turns_empty, _p(planes), _p(arrs[0]), _p(arrs[1]), _p(arrs[2]),
+                                    _p(out))
+    return out
+
+
+def render(planes, role, status, W, H, restrict_view=False, scale=32):
+    """render(mode="rgb_array", scale, draw_health=False) of observations -> u8 [B, W*s, H*s, 3]."""
+    planes = np.ascontiguousarray(planes, dtype=np.uint8)
+    B, S = planes.shape[0], planes.shape[3]
+    out = np.zeros((B, W * scale, H * scale, 3), np.uint8)
+    r = np.ascontiguousarray(role, dtype=np.uint8)
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    lib().wabo_render(B, W, H, S, int(bool(restrict_view)), scale, _p(planes), _p(r), _p(st), _p(out))
     return out
 
 

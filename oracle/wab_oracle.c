@@ -446,6 +446,62 @@ void wabo_featurize(int64_t B, int W, int H, int S, int turns_empty, const uint8
   }
 }
 
+/* render (wab_env.py:468-502), draw_health=False: channel c of cell (i, j) is 255 * grid_c;
+ * an empty cell is 127 when killed, else 255 and then every channel goes through mask_grid
+ * with the ostrich's role (:490-493: blind spots 0, only under restrict_view); each cell
+ * becomes a scale x scale block (:494).  The grids are the observation's (already masked,
+ * which mask_grid leaves unchanged). */
+void wabo_render(int64_t B, int W, int H, int S, int restrict_view, int scale, const uint8_t* planes,
+                 const uint8_t* role, const uint8_t* status, uint8_t* rgb) {
+  const int RW = W * scale, RH = H * scale;
+  for (int64_t e = 0; e < B; ++e) {
+    const uint8_t* pl = planes + (size_t)e * 3 * W * S;
+    const uint8_t(*m)[11] = role[e] == 1 ? GATHERER_MASK : LOOKOUT_MASK;
+    uint8_t* img = rgb + (size_t)e * RW * RH * 3;
+    for (int i = 0; i < W; ++i)
+      for (int j = 0; j < H; ++j) {
+        uint8_t c[3];
+        for (int k = 0; k < 3; ++k) c[k] = pl[k * W * S + i * S + j] ? 255 : 0;
+        if (!c[0] && !c[1] && !c[2]) c[0] = c[1] = c[2] = status[e] == 2 ? 127 : 255;
+        if (status[e] != 2 && restrict_view && i < 11 && j < 11 && m[i][j]) c[0] = c[1] = c[2] = 0;
+        for (int a = 0; a < scale; ++a)
+          for (int b2 = 0; b2 < scale; ++b2) {
+            uint8_t* px = img + ((size_t)(i * scale + a) * RH + (size_t)(j * scale + b2)) * 3;
+            px[0] = c[0];
+            px[1] = c[1];
+            px[2] = c[2];
+          }
+      }
+  }
+}
+
+int wabo_superbasic_dim(int W, int H, int turns_empty) {
+  const int md = W / 2 + H / 2 + 1;
+  return 4 * md + (turns_empty + 1) + 2 + 3;
+}
+
+/* SuperBasicObservationWrapper.observation (wab_env.py:914-927): the nearest bush of the bush
+ * grid (_get_nearest_things :763-810), food, role, status; flattened by gym 0.17 (each
+ * Discrete -> one-hot; the nearest-bush space is Discrete(max_distance), :906) */
+void wabo_featurize_superbasic(int64_t B, int W, int H, int S, int turns_empty, const uint8_t* planes,
+                               const uint8_t* food_turns, const uint8_t* role, const uint8_t* status,
+                               float* out) {
+  const int md = W / 2 + H / 2 + 1;
+  const int F = wabo_superbasic_dim(W, H, turns_empty);
+  for (int64_t i = 0; i < B; ++i) {
+    const uint8_t* pl = planes + (size_t)i * 3 * W * S;
+    float* o = out + (size_t)i * F;
+    memset(o, 0, sizeof(float) * (size_t)F);
+    int nb[4], sb[4], cb[4];
+    nearest_things(pl + W * S, W, H, S, md, nb, sb, cb);
+    int off = 0;
+    for (int k = 0; k < 4; ++k) { o[off + nb[k]] = 1.0f; off += md; }
+    o[off + food_turns[i]] = 1.0f; off += turns_empty + 1;
+    o[off + role[i]] = 1.0f; off += 2;
+    o[off + status[i]] = 1.0f;
+  }
+}
+
 /* actor_critic.finish_episode returns (actor_critic.py:139-143): per env, reverse
  * R = r + gamma * R in double (Python floats), restarting after each done; f32 out */
 void wabo_discounted_returns(int64_t T, int64_t B, const float* reward, const uint8_t* done,

@@ -1,9 +1,10 @@
-"""Golden vectors for the config-5 featurizer: the reference `PragmaticObsWrapper.observation`
-(wab_env.py:726-824) followed by gym 0.17's `spaces.flatten` (actor_critic.py:188).
+"""Golden vectors for the device featurizers: the reference `PragmaticObsWrapper.observation`
+(wab_env.py:726-824) and `SuperBasicObservationWrapper.observation` (:900-927), each followed
+by gym 0.17's `spaces.flatten` (actor_critic.py:188).
 
 Container-only (imports /root/reference through ref_harness).  Inputs are random wolf/bush
 grids of several densities plus the three hand-built grids of the reference's own KATs
-(wab_env_test.py:9-169); outputs are the wrapper's 11-tuple flattened to float32 [449].
+(wab_env_test.py:9-169); outputs are the wrappers' tuples flattened to float32 ([449] and [90] at 11x11).
 `flatten` is restated by the gym stub (gym is not installed): that layout is "parity
 unpinned" (SURVEY.md §8c); the wrapper's values themselves are pinned by the reference.
 
@@ -67,10 +68,15 @@ def main():
         grids.append(np.stack([w, b, o]))
         scal.append((rng.randint(41), rng.randint(2), rng.randint(3)))
         masks.append([np.zeros((11, 11)), LOOKOUT_MASK, GATHERER_MASK][rng.randint(3)])
-    feats = []
+    feats, sb_feats, sb_raw = [], [], []
+    superbasic = wab_env.SuperBasicObservationWrapper(env)
+    sb_space = superbasic.observation_space
     for g, (f, r, s), m in zip(grids, scal, masks):
         obs = (g[0], g[1], g[2], f, r, s, m)
         feats.append(gym.spaces.flatten(space, wrapper.observation(obs)))
+        sb = superbasic.observation(obs)
+        sb_raw.append(list(sb[0]) + [sb[1], sb[2], sb[3]])
+        sb_feats.append(gym.spaces.flatten(sb_space, sb))
     out = {
         "planes": np.stack(grids).astype(np.uint8),
         "scalars": np.asarray(scal, dtype=np.uint8),
@@ -80,6 +86,15 @@ def main():
     }
     np.savez_compressed(os.path.join(HERE, "pragmatic.npz"), **out)
     print("pragmatic.npz: %d cases, flatdim %d" % (len(feats), out["flatdim"]))
+    sb_out = {
+        "planes": out["planes"],
+        "scalars": out["scalars"],
+        "raw": np.asarray(sb_raw, dtype=np.int32),  # nearest_bush[4], food, role, status
+        "features": np.stack(sb_feats).astype(np.float32),
+        "flatdim": np.int64(gym.spaces.flatdim(sb_space)),
+    }
+    np.savez_compressed(os.path.join(HERE, "superbasic.npz"), **sb_out)
+    print("superbasic.npz: %d cases, flatdim %d" % (len(sb_feats), sb_out["flatdim"]))
 
 
 if __name__ == "__main__":

@@ -48,6 +48,23 @@ def test_oracle_featurizer_matches_reference_golden():
     assert np.array_equal(feats, z["features"])
 
 
+SUPERBASIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "superbasic.npz")
+
+
+def test_oracle_superbasic_matches_reference_golden():
+    """SuperBasicObservationWrapper (wab_env.py:900-927) + flatten, from the same inputs."""
+    z = np.load(SUPERBASIC)
+    feats = orc.featurize_superbasic(z["planes"], z["scalars"][:, 0], z["scalars"][:, 1], z["scalars"][:, 2],
+                                     11, 11)
+    assert feats.shape[1] == int(z["flatdim"]) == orc.superbasic_dim() == 90
+    assert np.array_equal(feats, z["features"])
+    # the one-hot groups decode to the wrapper's raw values
+    raw = z["raw"]
+    dec = np.stack([feats[:, 11 * k:11 * (k + 1)].argmax(1) for k in range(4)], 1)
+    assert np.array_equal(dec, raw[:, :4])
+    assert np.array_equal(feats[:, 44:85].argmax(1), raw[:, 4])
+
+
 def _returns_reference(rewards, gamma=0.99):
     R, out = 0, []
     for r in rewards[::-1]:          # actor_critic.py:139-143

@@ -240,6 +240,74 @@ def test_featurizer_on_env_obs_matches_oracle():
             assert np.array_equal(f.cpu().numpy(), want)
 
 
+def test_superbasic_matches_reference_golden_and_oracle():
+    """Device SuperBasicObservationWrapper + flatten == the reference wrapper's golden vectors,
+    and == the oracle on live env observations (31x31 included)."""
+    import torch
+
+    from oracle import oracle as orc
+    from wab_gym_amd.wrappers import SuperBasicObservationWrapper
+
+    z = np.load(gr.GOLDEN_DIR + "/superbasic.npz")
+    n = len(z["features"])
+    env = _env(None, n)
+    wrap = SuperBasicObservationWrapper(env)
+    assert wrap.feature_dim == int(z["flatdim"]) == 90
+    planes = torch.as_tensor(z["planes"]).cuda()
+    scal = torch.as_tensor(np.ascontiguousarray(z["scalars"].T)).cuda()
+    f = wrap.observation({"planes": planes, "scalars": scal})
+    assert np.array_equal(f.cpu().numpy(), z["features"])
+    for opts in (None, {"width": 31, "height": 31}):
+        env = _env(opts, 2000, validate_actions=False)
+        wrap = SuperBasicObservationWrapper(env)
+        wrap.reset()
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(2)
+        for _ in range(20):
+            f, r, d, _ = wrap.step(torch.randint(0, env.n_actions, (2000,), device="cuda:0", generator=g))
+            planes = env._obs["planes"].cpu().numpy()
+            sc = env._obs["scalars"].cpu().numpy()
+            want = orc.featurize_superbasic(planes, sc[0], sc[1], sc[2], env.W, env.H,
+                                            env.game_options["turns_to_empty_food"])
+            assert np.array_equal(f.cpu().numpy(), want)
+
+
+def test_render_matches_reference_frames_and_oracle():
+    """f3: device render == the reference's rgb_array frames (draw_health=False), and == the
+    oracle on live observations (31x31, restrict_view, killed envs)."""
+    import torch
+
+    from oracle import oracle as orc
+
+    z = np.load(gr.GOLDEN_DIR + "/render.npz")
+    names = bytes(z["set_names"]).decode().split(",")
+    scale = int(z["scale"])
+    for si, name in enumerate(names):
+        sel = z["set"] == si
+        n = int(sel.sum())
+        opts = {"restrict_view": True, "lookout_only": False} if name == "restrict" else None
+        env = _env(opts, n)
+        env.reset()
+        env._obs["planes"].copy_(torch.as_tensor(z["planes"][sel]))
+        env._obs["scalars"].copy_(torch.as_tensor(np.ascontiguousarray(z["scalars"][sel].T)))
+        img = env.render(scale=scale)
+        assert np.array_equal(img.cpu().numpy(), z["images"][sel]), name
+    for opts in (None, {"width": 31, "height": 31}, {"restrict_view": True, "lookout_only": False},
+                 {"chance_wolf_on_square": 0.05}):
+        env = _env(opts, 300, validate_actions=False)
+        env.reset()
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(3)
+        for _ in range(15):
+            env.step(torch.randint(0, env.n_actions, (300,), device="cuda:0", generator=g))
+        for scale in (1, 3):
+            img = env.render(scale=scale).cpu().numpy()
+            sc = env._obs["scalars"].cpu().numpy()
+            want = orc.render(env._obs["planes"].cpu().numpy(), sc[1], sc[2], env.W, env.H,
+                              env.game_options["restrict_view"], scale)
+            assert np.array_equal(img, want)
+
+
 def test_discounted_returns_match_oracle():
     import torch
 

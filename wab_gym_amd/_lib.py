@@ -16,6 +16,7 @@ EXPORTED = [
     "wab_abi_version", "wab_last_error", "wab_num_actions", "wab_create", "wab_destroy",
     "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
+    "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render",
 ]
 
 ABI_VERSION = 1
@@ -65,6 +66,9 @@ def load():
     L.wab_get_state.argtypes = [P, P, P, P, P, P, P, P]
     L.wab_feature_dim.argtypes = [P]
     L.wab_featurize.argtypes = [P, P, P, P, P]
+    L.wab_superbasic_dim.argtypes = [P]
+    L.wab_featurize_superbasic.argtypes = [P, P, P, P]
+    L.wab_render.argtypes = [P, P, I32, P, P]
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64

@@ -5,6 +5,7 @@
 // wab_step / wab_reset / wab_rollout, so they are safe to capture in a hipGraph.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -23,6 +24,7 @@ __global__ void wab_step_small(Params p);
 
 struct FeatParams {
   int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
+  int32_t kind;
   int64_t B;
   uint32_t mask_rows[2][11];
   const uint8_t* planes;
@@ -33,6 +35,16 @@ struct FeatParams {
   float* out;
 };
 __global__ void wab_featurize_kernel(FeatParams p);
+struct RenderParams {
+  int32_t W, H, S, OB, scale, restrict_view;
+  int64_t B;
+  uint32_t mask_rows[2][11];
+  const uint8_t* planes;
+  const uint8_t* role;
+  const uint8_t* status;
+  uint8_t* rgb;
+};
+__global__ void wab_render_kernel(RenderParams p);
 __global__ void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T, int64_t B,
                                    double gamma, const float* bootstrap, float* out);
 }
@@ -502,15 +514,16 @@ int wab_feature_dim(const wab_handle* h) {
   return 16 * (md + 1) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121;
 }
 
-int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
-                  void* stream) {
+namespace {
+int featurize(wab_handle* h, int kind, const wab_obs* obs, const uint8_t* view_mask, float* features, void* stream,
+              const char* what) {
   g_err.clear();
-  if (!h || !features) return fail(WAB_E_INVALID, "wab_featurize: NULL argument");
-  if (int rc = check_obs(obs, "wab_featurize")) return rc;
-  const int F = wab_feature_dim(h);
-  if (F < 0) return fail(WAB_E_INVALID, "wab_featurize: PragmaticObsWrapper cannot index this viewport");
+  if (!h || !features) return fail(WAB_E_INVALID, std::string(what) + ": NULL argument");
+  if (int rc = check_obs(obs, what)) return rc;
+  const int F = kind == 1 ? wab_superbasic_dim(h) : wab_feature_dim(h);
+  if (F < 0) return fail(WAB_E_INVALID, std::string(what) + ": the wrapper cannot index this viewport");
   if ((reinterpret_cast<uintptr_t>(features) & 15u) != 0)
-    return fail(WAB_E_INVALID, "wab_featurize: features must be 16-byte aligned");
+    return fail(WAB_E_INVALID, std::string(what) + ": features must be 16-byte aligned");
   const Params& p = h->p;
   wab::FeatParams fp;
   std::memset(&fp, 0, sizeof(fp));
@@ -519,6 +532,7 @@ int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, f
   fp.F = F;
   fp.turns_empty = p.turns_empty;
   fp.restrict_view = p.restrict_view;
+  fp.kind = kind;
   fp.B = p.B;
   std::memcpy(fp.mask_rows, p.mask_rows, sizeof(fp.mask_rows));
   fp.planes = obs->planes;
@@ -535,6 +549,59 @@ int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, f
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<void*>(&wab::wab_featurize_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(wab::wab_featurize_kernel, dim3(h->n_blocks), dim3(256), lds, (hipStream_t)stream, fp);
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+}  // namespace
+
+int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
+                  void* stream) {
+  return featurize(h, 0, obs, view_mask, features, stream, "wab_featurize");
+}
+
+int wab_superbasic_dim(const wab_handle* h) {
+  if (!h) return WAB_E_INVALID;
+  const Params& p = h->p;
+  return 4 * (p.W / 2 + p.H / 2 + 1) + (p.turns_empty + 1) + 2 + 3;
+}
+
+int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features, void* stream) {
+  return featurize(h, 1, obs, nullptr, features, stream, "wab_featurize_superbasic");
+}
+
+int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, void* stream) {
+  g_err.clear();
+  if (!h || !rgb) return fail(WAB_E_INVALID, "wab_render: NULL argument");
+  if (int rc = check_obs(obs, "wab_render")) return rc;
+  if (scale < 1 || scale > 256) return fail(WAB_E_INVALID, "wab_render: scale must be in [1, 256]");
+  const Params& p = h->p;
+  if ((uint64_t)p.W * scale * p.H * scale * 3 >= (1ull << 32))
+    return fail(WAB_E_INVALID, "wab_render: image too large");
+  wab::RenderParams rp;
+  std::memset(&rp, 0, sizeof(rp));
+  rp.W = p.W; rp.H = p.H; rp.S = p.S; rp.OB = p.OB;
+  rp.scale = scale;
+  rp.restrict_view = p.restrict_view;
+  rp.B = p.B;
+  std::memcpy(rp.mask_rows, p.mask_rows, sizeof(rp.mask_rows));
+  rp.planes = obs->planes;
+  rp.role = obs->role;
+  rp.status = obs->status;
+  rp.rgb = rgb;
+  if (p.B == 0) return WAB_OK;
+  const uint64_t per_env = (uint64_t)p.W * scale * p.H * scale * 3;
+  const uint64_t words = (per_env + 3) / 4;
+  const unsigned gx = (unsigned)std::min<uint64_t>((words + 255) / 256, 1024);
+  DeviceGuard guard(h->device);
+  for (int64_t e0 = 0; e0 < p.B; e0 += 65535) {  // grid.y is at most 65535 envs per launch
+    wab::RenderParams r2 = rp;
+    r2.planes = rp.planes + (size_t)e0 * p.OB;
+    r2.role = rp.role + e0;
+    r2.status = rp.status + e0;
+    r2.rgb = rp.rgb + (size_t)e0 * per_env;
+    r2.B = std::min<int64_t>(65535, p.B - e0);
+    hipLaunchKernelGGL(wab::wab_render_kernel, dim3(gx, (unsigned)r2.B), dim3(256), 0, (hipStream_t)stream, r2);
+  }
   HIP_TRY(hipGetLastError());
   return WAB_OK;
 }

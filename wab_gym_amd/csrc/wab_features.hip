@@ -1,7 +1,8 @@
 // wab_features.hip — config-5 device kernels for gfx950: the PragmaticObsWrapper
 // featurizer (+ gym 0.17 flatten) and the discounted-return scan of actor_critic.py.
 //
-// wab_featurize_kernel: one 256-thread workgroup per 64 envs.
+// wab_featurize_kernel: one 256-thread workgroup per 64 envs; `kind` selects the wrapper
+// (PragmaticObsWrapper, or SuperBasicObservationWrapper: nearest bush, food, role, status).
 //   phase 1  all threads   16-byte coalesced loads of the block's obs chunk, 1 byte -> 1 bit
 //                          into an LDS bit-stream (the inverse of the step kernel's phase F)
 //   phase 2  wave 0        lane = env: walk the set bits of the wolf and bush planes in
@@ -17,6 +18,7 @@ namespace wab {
 
 struct FeatParams {
   int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
+  int32_t kind;  // 0 PragmaticObsWrapper (:726-824), 1 SuperBasicObservationWrapper (:900-927)
   int64_t B;
   uint32_t mask_rows[2][11];
   const uint8_t* planes;
@@ -122,9 +124,21 @@ __global__ __launch_bounds__(256) void wab_featurize_kernel(FeatParams p) {
     const uint32_t ebit = (uint32_t)e * (uint32_t)p.OB;
     const uint32_t plane = (uint32_t)(p.W * p.S);
     int nw[4], sw[4], cw[4], nb[4], sb[4], cb[4];
+    uint32_t at = (uint32_t)e * (uint32_t)p.F;
+    if (p.kind == 1) {  // (nearest bush, food, role, status); nearest bush in Discrete(md) (:906)
+      scan_plane(p, in, ebit + plane, nb, sb, cb);
+      for (int k = 0; k < 4; ++k) {
+        fset(ob, at + (uint32_t)nb[k]);
+        at += (uint32_t)p.md;
+      }
+      fset(ob, at + p.food_turns[g]);
+      at += (uint32_t)(p.turns_empty + 1);
+      fset(ob, at + p.role[g]);
+      at += 2;
+      fset(ob, at + p.status[g]);
+    } else {
     scan_plane(p, in, ebit, nw, sw, cw);
     scan_plane(p, in, ebit + plane, nb, sb, cb);
-    uint32_t at = (uint32_t)e * (uint32_t)p.F;
     const int* groups[6] = {nw, sw, cw, nb, sb, cb};
     const int sizes[6] = {p.md + 1, p.md + 1, 11, p.md + 1, p.md + 1, 11};
     for (int q = 0; q < 6; ++q)
@@ -150,6 +164,7 @@ __global__ __launch_bounds__(256) void wab_featurize_kernel(FeatParams p) {
       for (int i = 0; i < 11; ++i)
         for (int j = 0; j < 11; ++j)
           if ((rows[i] >> j) & 1u) fset(ob, at + (uint32_t)(i * 11 + j));
+    }
     }
   }
   __syncthreads();

@@ -1,0 +1,63 @@
+// wab_render.hip — WolvesAndBushesEnv.render(mode="rgb_array", scale, draw_health=False)
+// (wab_env.py:468-502) for a batch, from the observation the step kernel wrote.
+//
+// rgb [B][W*scale][H*scale][3] u8: channel c of cell (i, j) is 255 * grid_c; an empty cell is
+// 127 when the ostrich was killed, else 255, and then mask_grid (restrict_view blind spots,
+// by role) zeroes it; each cell becomes a scale x scale block.  One thread per output dword
+// (4 bytes of consecutive pixels' channels), so stores coalesce; the text overlay of
+// draw_health=True (PIL's default font) is not reproduced.
+#include <hip/hip_runtime.h>
+
+#include "wab_params.h"
+
+namespace wab {
+
+struct RenderParams {
+  int32_t W, H, S, OB, scale, restrict_view;
+  int64_t B;
+  uint32_t mask_rows[2][11];
+  const uint8_t* planes;
+  const uint8_t* role;
+  const uint8_t* status;
+  uint8_t* rgb;
+};
+
+__device__ __forceinline__ uint8_t render_byte(const RenderParams& p, int64_t e, uint32_t o) {
+  const uint32_t RH = (uint32_t)(p.H * p.scale);
+  const uint32_t px = o / 3u, c = o - px * 3u;
+  const uint32_t row = px / RH, col = px - row * RH;
+  const int i = (int)(row / (uint32_t)p.scale), j = (int)(col / (uint32_t)p.scale);
+  const uint8_t* pl = p.planes + (size_t)e * p.OB + (size_t)(i * p.S + j);
+  const size_t plane = (size_t)p.W * p.S;
+  const bool w = pl[0] != 0, b = pl[plane] != 0, s = pl[2 * plane] != 0;
+  const bool killed = p.status[e] == 2;
+  if (!(w | b | s)) {
+    if (killed) return 127;
+    const int role = p.role[e] == 1 ? 1 : 0;
+    const bool blind = p.restrict_view && i < 11 && j < 11 && ((p.mask_rows[role][i] >> j) & 1u);
+    return blind ? 0 : 255;
+  }
+  const bool on = c == 0 ? w : c == 1 ? b : s;
+  return on ? 255 : 0;  // (objects never sit in blind spots: the observation is already masked)
+}
+
+__global__ __launch_bounds__(256) void wab_render_kernel(RenderParams p) {
+  const uint32_t per_env = (uint32_t)(p.W * p.scale) * (uint32_t)(p.H * p.scale) * 3u;
+  const uint32_t words = (per_env + 3u) / 4u;
+  const int64_t e = blockIdx.y;
+  if (e >= p.B) return;
+  uint8_t* out = p.rgb + (size_t)e * per_env;
+  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < words; q += gridDim.x * 256u) {
+    const uint32_t o = q * 4u;
+    if (o + 4u <= per_env && ((reinterpret_cast<uintptr_t>(out) & 3u) == 0)) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v |= (uint32_t)render_byte(p, e, o + k) << (8 * k);
+      *reinterpret_cast<uint32_t*>(out + o) = v;
+    } else {
+      for (uint32_t k = 0; k < 4u && o + k < per_env; ++k) out[o + k] = render_byte(p, e, o + k);
+    }
+  }
+}
+
+}  // namespace wab

@@ -168,6 +168,21 @@ class BatchedWolvesAndBushesEnv:
                    "wab_rollout")
         return planes, scal.permute(1, 0, 2), rew, done
 
+    def render(self, mode="rgb_array", scale=32, draw_health=False, out=None):
+        """render (wab_env.py:468-502) of every env's current observation on device:
+        u8 [B, W*scale, H*scale, 3].  Only mode "rgb_array" and draw_health=False (the
+        reference's food-count text uses PIL's default font, not reproduced)."""
+        if mode != "rgb_array":
+            raise NotImplementedError("only mode='rgb_array' (wab_env.py:104 metadata)")
+        if draw_health:
+            raise NotImplementedError("draw_health=True (PIL text overlay) is not reproduced")
+        t = self._torch
+        shape = (self.num_envs, self.W * scale, self.H * scale, 3)
+        img = t.empty(shape, dtype=t.uint8, device=self.device) if out is None else out
+        _lib.check(_lib.load().wab_render(self._h, ctypes.addressof(self._obs["struct"]), int(scale),
+                                          img.data_ptr(), self._stream()), "wab_render")
+        return img
+
     def counters(self):
         c = _lib.WabCounters()
         _lib.check(_lib.load().wab_get_counters(self._h, ctypes.addressof(c), self._stream()),

@@ -1,9 +1,11 @@
-"""Batched PragmaticObsWrapper and the actor-critic return scan (config 5).
+"""Batched observation wrappers and the actor-critic return scan (config 5).
 
 `PragmaticObsWrapper` mirrors the reference wrapper (wab_env.py:670-824) for a batched env:
 `observation(obs)` turns the batched 7-tuple into the wrapper's 11-tuple already flattened
 the way actor_critic.py feeds the policy (`gym.spaces.flatten`, actor_critic.py:188), i.e. a
 float32 tensor [B, 449] computed on device by one HIP kernel (wab_featurize).
+`SuperBasicObservationWrapper` (wab_env.py:900-927) does the same for its 4-tuple
+(nearest bush, food, role, status): float32 [B, 90] (wab_featurize_superbasic).
 """
 from __future__ import annotations
 
@@ -76,6 +78,45 @@ class PragmaticObsWrapper:
                 {"planes": t["planes"], "scalars": t["scalars"]},
                 out=self.env._torch.empty_like(self.features))
         return self.observation(), reward, done, info
+
+
+class SuperBasicObservationWrapper(PragmaticObsWrapper):
+    """SuperBasicObservationWrapper (wab_env.py:900-927): (nearest bush, food, role, status),
+    flattened by gym's rules (nearest bush 4 x Discrete(max_distance), :906)."""
+
+    def __init__(self, env):
+        self.env = env
+        lib = _lib.load()
+        self.feature_dim = int(lib.wab_superbasic_dim(env._h))
+        opts = env.game_options
+        self.max_distance = opts["width"] // 2 + opts["height"] // 2 + 1  # wab_env.py:903
+        md = self.max_distance
+        self.single_observation_space = Tuple((                          # wab_env.py:904-911
+            Tuple([Discrete(md)] * 4), Discrete(opts["turns_to_empty_food"] + 1), Discrete(2), Discrete(3)))
+        self.observation_space = Box(0.0, 1.0, (env.num_envs, self.feature_dim), dtype="float32")
+        self.action_space = env.action_space
+        self.spec = env.spec
+        t = env._torch
+        self.features = t.zeros((env.num_envs, self.feature_dim), dtype=t.float32, device=env.device)
+
+    def observation(self, obs=None, view_mask=None, out=None):
+        """Features of the env's current observation buffer (or of `obs`, as in
+        PragmaticObsWrapper.observation; the view mask is not part of this wrapper)."""
+        env = self.env
+        if obs is None:
+            st = env._obs["struct"]
+            keep = None
+        else:
+            planes = obs["planes"].contiguous()
+            scal = obs["scalars"].contiguous()
+            st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(),
+                             scal[2].data_ptr())
+            keep = (planes, scal)
+        dst = self.features if out is None else out
+        _lib.check(_lib.load().wab_featurize_superbasic(env._h, ctypes.addressof(st), dst.data_ptr(),
+                                                        env._stream()), "wab_featurize_superbasic")
+        del keep
+        return dst
 
 
 def discounted_returns(reward, done, gamma=0.99, bootstrap=None, out=None):
