@@ -24,6 +24,8 @@
  *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
  *   wab_featurize_superbasic <- SuperBasicObservationWrapper.observation wab_env.py:900-927
  *   wab_render            <- WolvesAndBushesEnv.render (rgb_array)   wab_env.py:468-502
+ *   wab_egocentric        <- WolvesAndBushesEnvEgoCentric._get_obs /  wab_env.py:930-979
+ *                            _get_bush_proximities                   wab_env.py:652-667
  *                            + gym.spaces.flatten                    actor_critic.py:188
  *   wab_discounted_returns<- finish_episode's return loop             actor_critic.py:139-143
  */
@@ -115,6 +117,7 @@ typedef struct wab_counters {
   uint64_t bad_actions;      /* actions outside [0, n_actions): treated as no-op */
   uint64_t steps;            /* env-steps executed */
   uint64_t resets;           /* env resets executed */
+  uint64_t ego_missing;      /* wab_egocentric calls that found a turn of the path unrecorded */
 } wab_counters;
 
 typedef struct wab_handle wab_handle;
@@ -198,6 +201,17 @@ int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features,
  * of an observation this handle produced: rgb [B][W*scale][H*scale][3] u8 device pointer.
  * The food-count text overlay of draw_health=True (PIL font) is not drawn. */
 int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, void* stream);
+
+/* Bush proximities of the egocentric env variants (WolvesAndBushesEnvEgoCentric and
+ * WolvesAndBushesEnvEgocentricJustBushes, wab_env.py:930-979) for the handle's current state:
+ * proximity u8 [B][5] (device), for the squares reached by up, right, down, left, stay:
+ * clip(md - d, 0, md), d = taxicab distance to the nearest food>0 bush among every tile seen
+ * this episode, md = width//2 + height//2 + 1 (<= 31 required); md for all five when no such
+ * bush exists (wab_env.py:664).  mask (device u8 [B], nullable) limits the envs written.
+ * The handle keeps a path of ostrich tiles for this: call it after EVERY wab_reset and
+ * wab_step of the envs it observes (turn t's entry is written at turn t); a missing entry
+ * counts in wab_counters.ego_missing.  Not valid after wab_rollout. */
+int wab_egocentric(wab_handle* h, const uint8_t* mask, uint8_t* proximity, void* stream);
 
 /* Discounted returns of actor_critic.finish_episode (actor_critic.py:139-143) over a
  * [T][B] rollout: R_t = r_t + gamma * R_{t+1}, restarted after every done_t, R_T =

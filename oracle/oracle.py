@@ -50,6 +50,7 @@ def lib():
                                   ctypes.c_int64, ctypes.c_uint32]
         L.wabo_feature_dim.argtypes = [ctypes.c_int] * 3
         L.wabo_featurize.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 6
+        L.wabo_egocentric.argtypes = [P, P]
         L.wabo_superbasic_dim.argtypes = [ctypes.c_int] * 3
         L.wabo_render.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 5 + [P] * 4
         L.wabo_featurize_superbasic.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 5
@@ -107,6 +108,12 @@ class OracleBatch:
                         _p(self.status), _p(self.reward), _p(self.done), _p(self.t_planes),
                         _p(self.t_food_turns), _p(self.t_role), _p(self.t_status), int(nthreads))
         return self.planes, self.food_turns, self.role, self.status, self.reward, self.done
+
+    def egocentric(self):
+        """Bush proximities u8 [B, 5] of the current state (wab_env.py:652-667)."""
+        out = np.zeros((self.B, 5), np.uint8)
+        lib().wabo_egocentric(self.h, _p(out))
+        return out
 
     def state(self):
         food = np.zeros(self.B, np.float64)

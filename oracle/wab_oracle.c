@@ -63,6 +63,11 @@ typedef struct {
   xy_t* wolves;
   int ne, cape;
   eaten_t* eaten;
+  /* tiles ever in view this episode (the rows of the reference's `bushes` table,
+   * generate_bushes wab_env.py:613-629): open-addressing set + insertion list */
+  int nseen, capseen;
+  uint64_t* seen_keys; /* capacity 2*capseen, 0 = empty */
+  xy_t* seen;
 } oenv;
 
 struct wabo_batch {
@@ -122,6 +127,50 @@ static void set_remaining(oenv* e, int32_t x, int32_t y, int rem) {
   e->ne++;
 }
 
+static uint64_t seen_key(int32_t x, int32_t y) {
+  return ((uint64_t)(uint32_t)(x + 0x40000000) << 32) | (uint32_t)(y + 0x40000000);
+}
+
+static void seen_insert_key(oenv* e, uint64_t k) {
+  const uint64_t m = 2 * (uint64_t)e->capseen - 1;
+  uint64_t i = (k * 0x9E3779B97F4A7C15ull) >> 17;
+  for (;; ++i)
+    if (e->seen_keys[i & m] == 0) { e->seen_keys[i & m] = k; return; }
+}
+
+/* a tile enters view: it joins the bush table once (wab_env.py:619 skips known tiles) */
+static void seen_add(oenv* e, int32_t x, int32_t y) {
+  const uint64_t k = seen_key(x, y);
+  if (e->capseen) {
+    const uint64_t m = 2 * (uint64_t)e->capseen - 1;
+    for (uint64_t i = (k * 0x9E3779B97F4A7C15ull) >> 17;; ++i) {
+      if (e->seen_keys[i & m] == k) return;
+      if (e->seen_keys[i & m] == 0) break;
+    }
+  }
+  if (e->nseen == e->capseen) { /* grow: list x2, table rebuilt at 2x the list */
+    e->capseen = e->capseen ? 2 * e->capseen : 256;
+    e->seen = (xy_t*)realloc(e->seen, sizeof(xy_t) * (size_t)e->capseen);
+    free(e->seen_keys);
+    e->seen_keys = (uint64_t*)calloc(2 * (size_t)e->capseen, sizeof(uint64_t));
+    for (int i = 0; i < e->nseen; ++i) seen_insert_key(e, seen_key(e->seen[i].x, e->seen[i].y));
+  }
+  seen_insert_key(e, k);
+  e->seen[e->nseen].x = x; e->seen[e->nseen].y = y;
+  e->nseen++;
+}
+
+static void seen_view(const wabo_batch* b, oenv* e) { /* visible_coords wab_env.py:510-525 */
+  const int cw = b->cfg.width / 2, ch = b->cfg.height / 2;
+  for (int tx = e->x - cw; tx <= e->x + cw; ++tx)
+    for (int ty = e->y - ch; ty <= e->y + ch; ++ty) seen_add(e, tx, ty);
+}
+
+static void seen_clear(oenv* e) {
+  if (e->capseen) memset(e->seen_keys, 0, 2 * (size_t)e->capseen * sizeof(uint64_t));
+  e->nseen = 0;
+}
+
 static void push_wolf(oenv* e, int32_t x, int32_t y) {
   if (e->nw == e->capw) {
     e->capw = e->capw ? 2 * e->capw : 8;
@@ -166,7 +215,12 @@ wabo_batch* wabo_create(const wab_config* cfg, int64_t batch, uint64_t seed, int
 
 void wabo_destroy(wabo_batch* b) {
   if (!b) return;
-  for (int64_t i = 0; i < b->batch; ++i) { free(b->envs[i].wolves); free(b->envs[i].eaten); }
+  for (int64_t i = 0; i < b->batch; ++i) {
+    free(b->envs[i].wolves);
+    free(b->envs[i].eaten);
+    free(b->envs[i].seen);
+    free(b->envs[i].seen_keys);
+  }
   free(b->envs);
   free(b->thresholds);
   free(b);
@@ -231,7 +285,9 @@ static void reset_one(wabo_batch* b, oenv* e, uint8_t* planes, uint8_t* food_tur
                 : c->starting_role;
   e->nw = 0;
   e->ne = 0;
-  /* generate_bushes :613-629 is implicit (tile function) */
+  /* generate_bushes :613-629: values are a tile function; only the seen set is kept */
+  seen_clear(e);
+  seen_view(b, e);
   if (c->wolves) { /* initialize_wolves :578-593: every visible tile, turn 0 */
     const int cw = c->width / 2, ch = c->height / 2;
     for (int tx = -cw; tx <= cw; ++tx)
@@ -263,7 +319,7 @@ static void step_one(wabo_batch* b, oenv* e, int a, uint8_t* planes, uint8_t* fo
     e->y += b->act_dy[a];
     if (b->act_role[a] >= 0) e->role = b->act_role[a];
   }
-  /* :259 generate_bushes — implicit */
+  seen_view(b, e); /* :259 generate_bushes (values implicit; the seen set grows) */
   /* :262-264 despawn: one draw per wolf in list order, keyed by its tile and its
    * occurrence index k among co-located wolves; decide all, then compact (stable) */
   {
@@ -472,6 +528,34 @@ void wabo_render(int64_t B, int W, int H, int S, int restrict_view, int scale, c
             px[2] = c[2];
           }
       }
+  }
+}
+
+/* WolvesAndBushesEnvEgoCentric._get_bush_proximities (wab_env.py:652-667), for the current
+ * state of every env: the 5 squares reachable by up/right/down/left/stay
+ * (generate_potential_actions :71-84), the taxicab distance d_k from each to the nearest
+ * food>0 bush of the whole seen world, clip(md - d_k, 0, md) with md = W//2 + H//2 + 1
+ * (:933-935); md for all five when no such bush exists (the Series([0]*5) branch :664). */
+void wabo_egocentric(const wabo_batch* b, uint8_t* out) {
+  static const int cx[5] = {0, 1, 0, -1, 0}, cy[5] = {1, 0, -1, 0, 0};
+  const int md = b->cfg.width / 2 + b->cfg.height / 2 + 1;
+  for (int64_t i = 0; i < b->batch; ++i) {
+    const oenv* e = &b->envs[i];
+    int best[5] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX};
+    int any = 0;
+    for (int s = 0; s < e->nseen; ++s) {
+      const int32_t tx = e->seen[s].x, ty = e->seen[s].y;
+      if (bush_remaining(b, e, tx, ty) <= 0) continue;
+      any = 1;
+      for (int k = 0; k < 5; ++k) {
+        const int d = abs(e->x + cx[k] - tx) + abs(e->y + cy[k] - ty);
+        if (d < best[k]) best[k] = d;
+      }
+    }
+    for (int k = 0; k < 5; ++k) {
+      const int v = any ? md - best[k] : md;
+      out[i * 5 + k] = (uint8_t)(v < 0 ? 0 : v > md ? md : v);
+    }
   }
 }
 

@@ -153,11 +153,12 @@ def load_reference():
     return _wab_env
 
 
-def make_env(seed: int, env_id: int, game_options=None):
-    """A reference `WolvesAndBushesEnv` whose draws are keyed by (seed, env_id, episode)."""
+def make_env(seed: int, env_id: int, game_options=None, cls="WolvesAndBushesEnv"):
+    """A reference `WolvesAndBushesEnv` (or the subclass named `cls`, e.g.
+    "WolvesAndBushesEnvEgoCentric") whose draws are keyed by (seed, env_id, episode)."""
     wab_env = load_reference()
 
-    class KeyedEnv(wab_env.WolvesAndBushesEnv):
+    class KeyedEnv(getattr(wab_env, cls)):
         def __init__(self, game_options):
             self._seed, self._env_id, self._episode = seed, env_id, -1
             super().__init__(game_options=game_options)

@@ -18,6 +18,10 @@ def __getattr__(name):
         from .env import BatchedWolvesAndBushesEnv
 
         return BatchedWolvesAndBushesEnv
+    if name in ("BatchedWolvesAndBushesEnvEgoCentric", "BatchedWolvesAndBushesEnvEgocentricJustBushes"):
+        from . import egocentric
+
+        return getattr(egocentric, name)
     if name == "PragmaticObsWrapper":
         from .wrappers import PragmaticObsWrapper
 

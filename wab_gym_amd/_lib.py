@@ -16,7 +16,7 @@ EXPORTED = [
     "wab_abi_version", "wab_last_error", "wab_num_actions", "wab_create", "wab_destroy",
     "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
-    "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render",
+    "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
 ]
 
 ABI_VERSION = 1
@@ -30,7 +30,7 @@ class WabObs(ctypes.Structure):
 class WabCounters(ctypes.Structure):
     _fields_ = [("wolf_overflow", ctypes.c_uint64), ("eaten_overflow", ctypes.c_uint64),
                 ("bad_actions", ctypes.c_uint64), ("steps", ctypes.c_uint64),
-                ("resets", ctypes.c_uint64)]
+                ("resets", ctypes.c_uint64), ("ego_missing", ctypes.c_uint64)]
 
 
 class WabError(RuntimeError):
@@ -69,6 +69,7 @@ def load():
     L.wab_superbasic_dim.argtypes = [P]
     L.wab_featurize_superbasic.argtypes = [P, P, P, P]
     L.wab_render.argtypes = [P, P, I32, P, P]
+    L.wab_egocentric.argtypes = [P, P, P, P]
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64

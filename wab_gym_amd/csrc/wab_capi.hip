@@ -45,6 +45,7 @@ struct RenderParams {
   uint8_t* rgb;
 };
 __global__ void wab_render_kernel(RenderParams p);
+__global__ void wab_egocentric_kernel(EgoParams p);
 __global__ void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T, int64_t B,
                                    double gamma, const float* bootstrap, float* out);
 }
@@ -61,6 +62,10 @@ struct wab_handle {
   size_t small_lds_bytes = 0;  // LDS of the small-view kernel
   bool reset_done = false;
   std::vector<void*> allocs;
+  // egocentric observation (allocated by the first wab_egocentric call)
+  uint4* ego_path = nullptr;
+  uint32_t* ego_diamond = nullptr;
+  int ego_cap = 0, ego_n_diamond = 0;
 };
 
 namespace {
@@ -476,6 +481,7 @@ int wab_get_counters(wab_handle* h, wab_counters* out, void* stream) {
   HIP_TRY(hipMemcpyAsync(br.data(), h->p.block_resets, br.size() * 8, hipMemcpyDeviceToHost,
                          (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  out->ego_missing = c[3];
   out->wolf_overflow = c[0];
   out->eaten_overflow = c[1];
   out->bad_actions = c[2];
@@ -602,6 +608,54 @@ int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, v
     r2.B = std::min<int64_t>(65535, p.B - e0);
     hipLaunchKernelGGL(wab::wab_render_kernel, dim3(gx, (unsigned)r2.B), dim3(256), 0, (hipStream_t)stream, r2);
   }
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+
+int wab_egocentric(wab_handle* h, const uint8_t* mask, uint8_t* proximity, void* stream) {
+  g_err.clear();
+  if (!h || !proximity) return fail(WAB_E_INVALID, "wab_egocentric: NULL argument");
+  if (!h->reset_done) return fail(WAB_E_STATE, "wab_egocentric: reset the handle first");
+  const Params& p = h->p;
+  const int Q = p.cw + p.ch + 1;
+  if (Q > 31) return fail(WAB_E_INVALID, "wab_egocentric: width//2 + height//2 must be <= 30");
+  DeviceGuard guard(h->device);
+  if (!h->ego_path) {
+    const int cap = p.max_turns + 129;  // + stepping on after done without a reset
+    std::vector<uint32_t> dia;
+    for (int dy = -Q; dy <= Q; ++dy)
+      for (int dx = -Q; dx <= Q; ++dx)
+        if (std::abs(dx) + std::abs(dy) <= Q) dia.push_back(((uint32_t)dx & 0xFFu) | (((uint32_t)dy & 0xFFu) << 8));
+    void* path = nullptr;
+    void* d = nullptr;
+    const size_t path_bytes = (size_t)cap * (size_t)(p.B > 0 ? p.B : 1) * 16;
+    if (hipMalloc(&path, path_bytes) != hipSuccess) return fail(WAB_E_NOMEM, "wab_egocentric: hipMalloc");
+    h->allocs.push_back(path);
+    if (hipMalloc(&d, dia.size() * 4) != hipSuccess) return fail(WAB_E_NOMEM, "wab_egocentric: hipMalloc");
+    h->allocs.push_back(d);
+    HIP_TRY(hipMemcpy(d, dia.data(), dia.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemsetAsync(path, 0xFF, path_bytes, (hipStream_t)stream));  // episode 0xFFFFFFFF: unset
+    h->ego_path = (uint4*)path;
+    h->ego_diamond = (uint32_t*)d;
+    h->ego_cap = cap;
+    h->ego_n_diamond = (int)dia.size();
+  }
+  if (p.B == 0) return WAB_OK;
+  wab::EgoParams ep;
+  std::memset(&ep, 0, sizeof(ep));
+  ep.cw = p.cw; ep.ch = p.ch; ep.Q = Q;
+  ep.cap = h->ego_cap;
+  ep.n_diamond = h->ego_n_diamond;
+  ep.eaten_cap = p.eaten_cap;
+  ep.bush_th = p.bush_th; ep.bush_tl = p.bush_tl;
+  ep.seed = p.seed; ep.env_base = p.env_base; ep.B = p.B;
+  ep.hdr = p.hdr; ep.eaten_xy = p.eaten_xy; ep.eaten_rem = p.eaten_rem;
+  ep.diamond = h->ego_diamond;
+  ep.path = h->ego_path;
+  ep.mask = mask;
+  ep.out = proximity;
+  ep.counters = p.counters;
+  hipLaunchKernelGGL(wab::wab_egocentric_kernel, dim3((unsigned)p.B), dim3(64), 0, (hipStream_t)stream, ep);
   HIP_TRY(hipGetLastError());
   return WAB_OK;
 }

@@ -147,4 +147,24 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   return L;
 }
 
+// Egocentric bush proximities (wab_egocentric.hip): reads the step's per-env state and keeps
+// a per-env path of ostrich tiles, one entry per turn of the current episode.
+struct EgoParams {
+  int32_t cw, ch, Q;        // Q = max_distance = W//2 + H//2 + 1 (wab_env.py:933-935), <= 31
+  int32_t cap;              // path entries per env
+  int32_t n_diamond;        // tiles with |dx| + |dy| <= Q
+  int32_t eaten_cap;
+  uint32_t bush_th, bush_tl;
+  uint64_t seed;
+  int64_t env_base, B;
+  const uint4* hdr;
+  const uint32_t* eaten_xy;
+  const uint8_t* eaten_rem;
+  const uint32_t* diamond;  // [n_diamond] packed (dx, dy) int8 offsets
+  uint4* path;              // [cap][B] {ostrich tile, food>0 tiles seen so far, episode, 0}
+  const uint8_t* mask;      // nullable: only envs with mask[i] != 0
+  uint8_t* out;             // [B][5]
+  unsigned long long* counters;  // [3]: path entries missing (stale or beyond cap)
+};
+
 }  // namespace wab
