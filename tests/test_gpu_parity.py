@@ -87,6 +87,43 @@ def test_c3_batch65536_wide31_padded_lockstep():
     _lockstep({"width": 31, "height": 31}, 65536, 12, stride=32)
 
 
+@pytest.mark.parametrize("opts,stride,slots,autoreset", [
+    ({"width": 31, "height": 31}, 32, 16, True),
+    ({"width": 31, "height": 31, "chance_wolf_on_square": 0.01, "wolf_chance_to_despawn": 0.2,
+      "wolf_spawn_margin": 2}, 32, 32, True),
+    ({"width": 17, "height": 13, "lookout_only": False}, 16, 8, True),
+    ({"width": 25, "height": 29, "starting_food": None, "starting_role": None}, 32, 16, True),
+    ({"width": 31, "height": 15, "wolves_can_move": False, "god_mode": True}, 16, 8, True),
+    ({"width": 13, "height": 11, "turns_to_fill_food": 4, "max_turns": 60, "bush_power": 60}, 16, 8, True),
+    ({"width": 31, "height": 31}, 32, 16, False),
+])
+def test_wide_kernel_lockstep(opts, stride, slots, autoreset):
+    """The wide-view kernel (W, H <= 32, rows of 16 or 32 bytes) against the oracle."""
+    env, _ = _lockstep(opts, 1000, 120, autoreset=autoreset, stride=stride, wolf_slots=slots, base=5)
+    assert env.step_kernel == "wide"
+
+
+def test_wide_kernel_reset_mask():
+    import torch
+
+    opts = {"width": 31, "height": 31}
+    env = _env(opts, 300, plane_stride=32, wolf_slots=16)
+    orc = _oracle(opts, 300, stride=32)
+    env.reset()
+    orc.reset()
+    rng = np.random.RandomState(9)
+    for t in range(30):
+        a = rng.randint(5, size=300)
+        env.step(torch.as_tensor(a))
+        orc.step(a)
+        if t % 10 == 9:
+            mask = (rng.random_sample(300) < 0.3).astype(np.uint8)
+            env.reset(torch.as_tensor(mask))
+            orc.reset(mask)
+        assert np.array_equal(env._obs["planes"].cpu().numpy(), orc.planes), t
+    assert np.array_equal(env.state()["episode"], orc.state()["episode"])
+
+
 def test_headline_batch65536_default_lockstep():
     _lockstep(None, 65536, 40)
 

@@ -21,6 +21,8 @@ template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
 template <int SLOTS>
 __global__ void wab_step_small(Params p);
+template <int MODE, int SLOTS>
+__global__ void wab_step_wide(Params p);
 
 struct FeatParams {
   int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
@@ -137,12 +139,28 @@ bool small_map(const Params& p) { return p.WHW <= 4; }
 
 // Step kernels.  The block kernel (wab_step.hip) handles every configuration; views whose
 // planes fit 128 bits (W*H <= 128, unpadded rows, spawn ring <= 128 tiles, restrict_view only
-// at exactly 11x11) step with the four-wave small-view kernel (wab_step_small.hip).
-// WAB_STEP_KERNEL=block selects the block kernel for those too (A/B measurements).
-enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1 };
+// at exactly 11x11) step with the four-wave small-view kernel (wab_step_small.hip); other
+// views of at most 32 x 32 cells in rows of 16 or 32 bytes without restrict_view step and
+// reset with the wide-view kernel (wab_step_wide.hip, its own bitmap layout: one dword per
+// row).  WAB_STEP_KERNEL=block selects the block kernel for all (A/B measurements).
+enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1, KERNEL_WIDE = 2 };
 
 bool small_view(const Params& p) {
   return p.WH <= 128 && p.S == p.H && p.R <= 128 && (!p.restrict_view || (p.W == 11 && p.H == 11));
+}
+
+bool wide_view(const Params& p) {
+  return !small_view(p) && p.W <= 32 && p.H <= 32 && (p.S == 16 || p.S == 32) && p.S >= p.H &&
+         !p.restrict_view && wab::wide_layout(p).total * 4u <= 64u * 1024u;
+}
+
+template <int MODE>
+void* wide_kernel_ptr(int slots) {
+  switch (slots) {
+    case 8: return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, 8>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, 16>);
+    default: return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, 32>);
+  }
 }
 
 void* small_kernel_ptr(int slots) {
@@ -156,7 +174,15 @@ void* small_kernel_ptr(int slots) {
 template <int MODE>
 int launch(wab_handle* h, const Params& p, hipStream_t stream) {
   if (h->n_blocks == 0) return WAB_OK;
-  if (MODE == 0 && h->step_kernel == KERNEL_SMALL) {
+  if (h->step_kernel == KERNEL_WIDE) {
+    const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
+    const size_t lds = (size_t)wab::wide_layout(p).total * 4u;
+    switch (h->slots) {
+      case 8: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 8>), grid, block, lds, stream, p); break;
+      case 16: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 16>), grid, block, lds, stream, p); break;
+      default: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 32>), grid, block, lds, stream, p); break;
+    }
+  } else if (MODE == 0 && h->step_kernel == KERNEL_SMALL) {
     const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
     switch (h->slots) {
       case 8: hipLaunchKernelGGL(wab::wab_step_small<8>, grid, block, h->small_lds_bytes, stream, p); break;
@@ -203,7 +229,7 @@ int64_t wab_batch(const wab_handle* h) { return h ? h->p.B : 0; }
 
 const char* wab_step_kernel(const wab_handle* h) {
   if (!h) return "";
-  return h->step_kernel == KERNEL_SMALL ? "small" : "block";
+  return h->step_kernel == KERNEL_SMALL ? "small" : h->step_kernel == KERNEL_WIDE ? "wide" : "block";
 }
 
 int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id_base, int device,
@@ -254,6 +280,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   p.WHW = (p.WH + 31) / 32;
   p.SL = p.W > p.H ? p.W : p.H;
   p.magic_OB = (uint32_t)((1ull << 32) / (uint64_t)p.OB) + 1u;
+  p.magic_CPE = p.OB >= 16 ? (uint32_t)((1ull << 32) / (uint64_t)(p.OB / 16)) + 1u : 1u;
   p.n_actions = n_actions_of(c);
   for (int a = 0; a < 6; ++a) p.act_role[a] = -1;  // moves: wab::decode_action (up right down left)
   if (c->gatherer_only) p.act_role[4] = 1;       // wab_env.py:149-159
@@ -311,7 +338,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   h->lds_bytes = (size_t)wab::lds_layout(p, slots).total * 4u;
   {
     const char* k = std::getenv("WAB_STEP_KERNEL");
-    h->step_kernel = small_view(p) && !(k && std::strcmp(k, "block") == 0) ? KERNEL_SMALL : KERNEL_BLOCK;
+    const bool forced_block = k && std::strcmp(k, "block") == 0;
+    h->step_kernel = forced_block ? KERNEL_BLOCK : small_view(p) ? KERNEL_SMALL : wide_view(p) ? KERNEL_WIDE : KERNEL_BLOCK;
     h->small_lds_bytes = (size_t)wab::small_layout(p).total * 4u;
   }
   if (h->lds_bytes > 160u * 1024u) {
@@ -334,7 +362,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   rc |= alloc((void**)&p.wolves, B * 4 * (size_t)slots);
   rc |= alloc((void**)&p.eaten_xy, B * 4 * (size_t)cap);
   rc |= alloc((void**)&p.eaten_rem, B * (size_t)cap);
-  rc |= alloc((void**)&p.bushmap, B * 4 * (size_t)p.WHW);
+  rc |= alloc((void**)&p.bushmap, B * 4 * (size_t)(p.WHW > p.W ? p.WHW : p.W));  // (wide: W rows)
   rc |= alloc((void**)&p.counters, 4 * 8);
   rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   uint64_t* thr = nullptr;
@@ -382,6 +410,11 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
                   kernel_ptr<1, false>(slots)})
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
+  if (h->step_kernel == KERNEL_WIDE)
+    for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots)})
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(wab::wide_layout(p).total * 4u));
   if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
     e = hipFuncSetAttribute(small_kernel_ptr(slots), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)h->small_lds_bytes);

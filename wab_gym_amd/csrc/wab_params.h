@@ -41,6 +41,7 @@ struct Params {
   int32_t RW, WHW;          // dwords of a ring mask / of a WH mask (WHW = bush bitmap words)
   int32_t SL;               // strip slots per env = max(W, H) (tiles entering the view on a move)
   uint32_t magic_OB;        // floor(2^32 / OB) + 1 (division helper)
+  uint32_t magic_CPE;       // the same for OB / 16 (16-byte obs chunks per env, wide kernel)
   // ---- rules
   int32_t n_actions;
   int32_t act_role[6];      // role set by each action, -1 = NaN (unchanged); moves: decode_action()
@@ -143,6 +144,34 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.jbm = o; o += 64u * 4u;
   L.jwm = o; o += 64u * 4u;  // (directly after jbm: zeroed together)
   L.jkey = o; o += 2u * 2u * 64u;
+  L.total = o;
+  return L;
+}
+
+// LDS of the wide-view step (wab_step_wide.hip; W, H <= 32, rows of S = 16 or 32 bytes):
+// one 64-env group per workgroup, view bitmaps as one dword per row (bit j = column j),
+// env-major with a 33-dword pitch so that lanes (= envs) touching the same row hit
+// different banks (dwords)
+constexpr uint32_t kWidePitch = 33;
+struct WideLayout {
+  uint32_t bm, wp, spawn, spw, thr, cval, info, blk, jobEnv, jobKey, total;
+};
+
+__host__ __device__ inline WideLayout wide_layout(const Params& p) {
+  WideLayout L;
+  uint32_t o = 0;
+  L.bm = o; o += 64u * kWidePitch + 4u;       // bush bitmaps (snapshot, pre-eat)
+  o = lds_align4(o);
+  L.wp = o; o += 64u * kWidePitch + 4u;       // wolf grids
+  o = lds_align4(o);
+  L.spw = (((uint32_t)p.R + 31u) >> 5) | 1u;  // spawn-mask dwords per env (odd pitch)
+  L.spawn = o; o += lds_align4(64u * L.spw);
+  L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
+  L.cval = o; o += 64u;                       // generated berries of the ostrich's tile
+  L.info = o; o += 64u;                       // W0 -> all: job | emptied << 1
+  L.blk = o; o += 4u;                         // n_jobs, job mask lo, hi
+  L.jobEnv = o; o += 64u;
+  L.jobKey = o; o += 128u;
   L.total = o;
   return L;
 }

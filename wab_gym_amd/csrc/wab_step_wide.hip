@@ -1,0 +1,607 @@
+// wab_step_wide.hip — the fused step (and reset) for wide views: W, H <= 32 with rows of
+// S = 16 or 32 bytes, no restrict_view (the 31x31-in-32x32 configuration C3 of SURVEY.md).
+//
+// At 31x31 the step is dominated by its output: 2976 obs bytes per env against ~230 bytes
+// of state, so the kernel is organised around getting the obs stores out early and at full
+// width.  One 256-thread workgroup serves 64 envs; each wave runs one lane per env:
+//
+//          W0 dynamics            W1 bushes               W2, W3 ring
+//   P0     state + log loads,     bitmap rows (one dword  zero the wolf grids,
+//          despawn, pursuit,      per row), scroll,       spawn-ring draws
+//          kill                   entering row/column
+//                                 draws, emptied tiles,
+//                                 ostrich-tile value
+//   -- B1 --
+//   P1     wolf grid, eat, hunger, starve, reward/done, scalars, job list
+//   -- B2 --
+//   P2     W0: spawns, state stores; all: obs chunks (16 bytes: one row half of one plane)
+//          of the continuing envs (+ terminal obs), bitmap stores
+//   (done envs: B3, reset draws by ballot, B4, new episodes, their obs and bitmaps)
+//
+// The view bitmaps live in LDS as one dword per row (bit j = column j): the move scrolls
+// them by a row index (x moves) or a shift (y moves), the entering strip is one row word or
+// one bit per row, and an obs chunk is 16 bits of one row expanded to 16 bytes.  Every obs
+// store wave-instruction writes 1 KiB contiguous.  Reset (MODE_RESET) is the done-env path
+// alone, so the bitmap layout stays private to this kernel.
+#include <hip/hip_runtime.h>
+
+#include "wab_small.h"
+
+namespace wab {
+
+#ifdef WAB_STAMPS
+#define WIDE_STAMP(slot)                                                                 \
+  do {                                                                                   \
+    if (lane == 0 && p.stamps)                                                           \
+      p.stamps[(size_t)blockIdx.x * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#else
+#define WIDE_STAMP(slot) do {} while (0)
+#endif
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// header, action, the move (:252-258) and the episode key: read by every wave
+struct WHead {
+  bool active, valid_action;
+  uint4 hdr;
+  int32_t ox, oy, turn;
+  int dir, role;
+  uint32_t cpos, b0, b1;
+  uint64_t kenv;
+};
+
+template <int MODE>
+__device__ __forceinline__ WHead whead(const Params& p, int64_t g, bool active) {
+  WHead h;
+  h.active = active;
+  h.hdr = make_uint4(0u, 0u, 0u, 0u);
+  int a = 0;
+  if (active) {
+    h.hdr = p.hdr[g];
+    if (MODE == MODE_STEP) a = (int)p.actions[g];
+  }
+  h.kenv = env_key(p.seed, (uint64_t)(p.env_base + g));  // overlaps the loads
+  h.ox = xy_x(h.hdr.x);
+  h.oy = xy_y(h.hdr.x);
+  h.turn = (int32_t)h.hdr.y + 1;
+  h.role = (int)misc_role(h.hdr.z);
+  h.dir = DIR_STAY;
+  h.valid_action = true;
+  if (MODE == MODE_STEP) {
+    h.valid_action = a >= 0 && a < p.n_actions;
+    if (h.valid_action) {
+      int dx, dy, nr;
+      decode_action(p, a, dx, dy, nr);
+      h.ox += dx;
+      h.oy += dy;
+      h.dir = dx > 0 ? DIR_RIGHT : dx < 0 ? DIR_LEFT : dy > 0 ? DIR_UP : dy < 0 ? DIR_DOWN : DIR_STAY;
+      if (nr >= 0) h.role = nr;
+    }
+  }
+  h.cpos = xy_pack(h.ox, h.oy);
+  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
+  h.b0 = (uint32_t)ek;
+  h.b1 = (uint32_t)(ek >> 32);
+  return h;
+}
+
+// bush bits of the row (x moves: bit j) or column (y moves: bit i) that scrolled into view
+// (generate_bushes :613-629); cell (i, j) is world (ox + cw - i, oy + ch - j)
+__device__ __forceinline__ uint32_t strip_bits(const Params& p, const WHead& h) {
+  if (h.dir == DIR_STAY) return 0u;
+  const bool horiz = h.dir == DIR_RIGHT || h.dir == DIR_LEFT;
+  const int n = horiz ? p.H : p.W;
+  const int i0 = h.dir == DIR_LEFT ? p.W - 1 : 0, j0 = h.dir == DIR_DOWN ? p.H - 1 : 0;
+  const uint32_t ts = make_ts(SITE_BUSH, 0, 0), hk = ts ^ h.b1;
+  uint32_t bits = 0;
+  for (int c = 0; c < n; c += 4) {
+    uint32_t h1[4], hh[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = horiz ? i0 : c + k, j = horiz ? c + k : j0;
+      h1[k] = xy_pack(h.ox + p.cw - i, h.oy + p.ch - j) ^ h.b0;
+    }
+    fmix32x4(h1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hh[k] = h1[k] ^ hk;
+    fmix32x4(hh);
+    uint32_t hit = 0, tie = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hit |= (hh[k] > p.bush_th ? 1u : 0u) << k;
+      tie |= (hh[k] == p.bush_th ? 1u : 0u) << k;
+    }
+    const uint32_t in = n - c >= 4 ? 0xFu : (1u << (n - c)) - 1u;
+    if (tie & in) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, h.b0) >= p.bush_tl) hit |= 1u << k;
+    }
+    bits |= (hit & in) << c;
+  }
+  return bits;
+}
+
+// spawn draws (spawn_wolves :527-576, wolf iff u < p/2) of ring tiles [32 w, 32 w + 32)
+__device__ __forceinline__ uint32_t ring_word(const Params& p, const WHead& h, int w) {
+  const int r0 = 32 * w, r1 = min(p.R, r0 + 32);
+  const uint32_t ts = make_ts(SITE_SPAWN, 0, h.turn), hk = ts ^ h.b1;
+  const uint4* ring = reinterpret_cast<const uint4*>(p.tables + p.ring_at);  // uniform: scalar loads
+  uint32_t bits = 0;
+  for (int r = r0; r < r1; r += 4) {
+    const uint4 o = ring[r >> 2];  // padded to a multiple of 4 entries
+    uint32_t h1[4] = {xy_add(h.cpos, o.x) ^ h.b0, xy_add(h.cpos, o.y) ^ h.b0, xy_add(h.cpos, o.z) ^ h.b0,
+                      xy_add(h.cpos, o.w) ^ h.b0};
+    fmix32x4(h1);
+    uint32_t hh[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hh[k] = h1[k] ^ hk;
+    fmix32x4(hh);
+    uint32_t hits = 0, tie = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hits |= (hh[k] < p.spawn_th ? 1u : 0u) << k;
+      tie |= (hh[k] == p.spawn_th ? 1u : 0u) << k;
+    }
+    if (tie) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, h.b0) < p.spawn_tl) hits |= 1u << k;
+    }
+    hits &= r + 4 <= r1 ? 0xFu : (1u << (r1 - r)) - 1u;
+    bits |= hits << (r - r0);
+  }
+  return bits;
+}
+
+// 16 cells of one row -> 16 bytes
+__device__ __forceinline__ u32x4 expand16(uint32_t v) {
+  u32x4 q;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+  return q;
+}
+
+// obs chunk r (16 bytes) of env e: plane k (wolf, bush, ostrich), row i, half
+__device__ __forceinline__ uint32_t chunk_bits(const Params& p, const uint32_t* bm, const uint32_t* wp, uint32_t e,
+                                               uint32_t r) {
+  const uint32_t CPR = (uint32_t)p.S >> 4, WC = (uint32_t)p.W * CPR;
+  const uint32_t k = (r >= WC ? 1u : 0u) + (r >= 2u * WC ? 1u : 0u);
+  const uint32_t r2 = r - k * WC;
+  const uint32_t i = CPR == 2u ? r2 >> 1 : r2;
+  const uint32_t half = CPR == 2u ? r2 & 1u : 0u;
+  const uint32_t* rows = k == 0u ? wp : bm;
+  uint32_t row = rows[e * kWidePitch + i];
+  if (k == 2u) row = i == (uint32_t)p.cw ? 1u << p.ch : 0u;  // the ostrich grid: self only
+  return (row >> (16u * half)) & 0xFFFFu;
+}
+
+}  // namespace
+
+template <int MODE, int SLOTS>
+__global__ __launch_bounds__(256) void wab_step_wide(Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const WideLayout L = wide_layout(p);
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  if (g0 >= p.B) return;  // (uniform over the workgroup)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n_active = (int)min((int64_t)64, p.B - g0);
+  const int64_t g = g0 + lane;
+  const bool active = lane < n_active;
+  uint32_t* bm = lds + L.bm;
+  uint32_t* wp = lds + L.wp;
+  uint32_t* spawn = lds + L.spawn;
+  uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr);
+  uint32_t* cval = lds + L.cval;
+  uint32_t* info = lds + L.info;
+  uint32_t* blk = lds + L.blk;
+  uint32_t* jobEnv = lds + L.jobEnv;
+  uint32_t* jobKey = lds + L.jobKey;
+  constexpr uint32_t P = kWidePitch;
+  const uint32_t OB = (uint32_t)p.OB, CPE = OB >> 4;
+  const uint32_t me = (uint32_t)lane * P;
+
+  const WHead h = whead<MODE>(p, g, active);
+
+  // W0's per-env state (lane = env)
+  double food = 0.0;
+  uint32_t wr[SLOTS];
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
+  uint32_t live = 0;
+  int status = 0, ne = 0, ndep = 0;
+  bool job = false, emptied = false;
+  unsigned long long eaten_of = 0, wolf_of = 0;
+
+  if constexpr (MODE == MODE_STEP) {
+    WIDE_STAMP(8 * wave);
+    if (wave == 0) {
+      // ------------------------------------------------ W0 P0: loads, despawn, pursuit, kill
+      __builtin_amdgcn_s_setprio(3);  // the longest chain
+      uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
+      if (active) {
+        food = p.food[g];
+#pragma unroll
+        for (int k = 0; k < 4 && k < SLOTS; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < p.eaten_cap) {
+            lxy[i] = p.eaten_xy[(int64_t)i * p.B + g];
+            lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
+          }
+      }
+      const int nw = (int)misc_nw(h.hdr.z);
+      ne = (int)misc_ne(h.hdr.z);
+      ndep = (int)misc_ndep(h.hdr.z);
+      const int status_old = (int)misc_status(h.hdr.z);
+#pragma unroll
+      for (int k = 4; k < SLOTS; ++k)
+        if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
+      live = nw >= 32 ? ~0u : ((1u << nw) - 1u);
+      // despawn (:262-264): one draw per wolf, keyed by its tile and its occurrence index
+      // among the co-located wolves before it; groups of 4 slots
+      {
+        uint32_t keep = 0;
+#pragma unroll
+        for (int g4 = 0; g4 < SLOTS; g4 += 4) {
+          const uint32_t live4 = (live >> g4) & 0xFu;
+          if (!live4) continue;
+          uint32_t h1[4], hh[4], ts[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int k = g4 + q;
+            uint32_t occ = 0;
+#pragma unroll
+            for (int t = 0; t < k; ++t) occ += (((live >> t) & 1u) && wr[t] == wr[k]) ? 1u : 0u;
+            ts[q] = make_ts(SITE_DESPAWN, occ, h.turn);
+            h1[q] = wr[k] ^ h.b0;
+          }
+          fmix32x4(h1);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hh[q] = h1[q] ^ ts[q] ^ h.b1;
+          fmix32x4(hh);
+          uint32_t kp = 0, tie = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            kp |= (hh[q] > p.keep_th ? 1u : 0u) << q;
+            tie |= (hh[q] == p.keep_th ? 1u : 0u) << q;
+          }
+          if (tie & live4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (((tie >> q) & 1u) && draw_lo21(h1[q], ts[q], h.b0) >= p.keep_tl) kp |= 1u << q;
+          }
+          keep |= (kp & live4) << g4;
+        }
+        live = keep;
+      }
+      // pursuit (:267-286): one axis step toward the ostrich, ties along x; kill (:291-297)
+      bool kill = false;
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) {
+        if (!((live >> k) & 1u)) continue;
+        int wx = xy_x(wr[k]), wy = xy_y(wr[k]);
+        if (p.wolves_can_move) {
+          const int ddx = h.ox - wx, ddy = h.oy - wy;
+          const bool alongx = abs(ddx) >= abs(ddy);
+          wx += alongx ? sgn(ddx) : 0;
+          wy += alongx ? 0 : sgn(ddy);
+          wr[k] = xy_pack(wx, wy);
+        }
+        kill |= wx == h.ox && wy == h.oy;
+      }
+      kill = kill && !p.god_mode;
+      // eaten log, first entries: the ostrich's tile
+      int found = -1, found_rem = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < ne && lxy[k] == h.cpos) { found = k; found_rem = (int)lrem[k]; }
+      WIDE_STAMP(1);
+      lds_barrier();  // B1: bitmap rows, the ostrich-tile value, zeroed wolf grids
+      WIDE_STAMP(2);
+      // ------------------------------------------------ W0 P1: grid of S, eat, starve, done
+      double reward = 0.0;
+      if (active) {
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k) {  // wolf grid (:412-428), snapshot #2
+          if (!((live >> k) & 1u)) continue;
+          const int ddx = h.ox - xy_x(wr[k]), ddy = h.oy - xy_y(wr[k]);
+          if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
+        }
+        const bool center_bush = ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u) != 0u;
+        if (center_bush && found < 0 && ne > 4) {
+          for (int i = 4; i < ne; ++i)
+            if (p.eaten_xy[(int64_t)i * p.B + g] == h.cpos) { found = i; found_rem = (int)p.eaten_rem[(int64_t)i * p.B + g]; }
+        }
+        const int rem = found >= 0 ? found_rem : (center_bush ? (int)cval[lane] : 0);
+        if (rem > 0 && status_old == 0 && (h.role == 1 || p.lookout_only)) {  // eat (:299-313)
+          food = food + p.fill;
+          food = food < 0.0 ? 0.0 : (food > 1.0 ? 1.0 : food);
+          reward += p.r_eat;
+          bool logged = true;
+          if (found >= 0) {
+            p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
+          } else if (ne < p.eaten_cap) {
+            p.eaten_xy[(int64_t)ne * p.B + g] = h.cpos;
+            p.eaten_rem[(int64_t)ne * p.B + g] = (uint8_t)(rem - 1);
+            ne += 1;
+          } else {
+            eaten_of += 1;
+            logged = false;
+          }
+          if (rem == 1) {  // emptied: gone from the cached view from the next step on
+            emptied = true;
+            if (logged) ndep += 1;
+          }
+        }
+        food = food - p.hunger;  // :316-322
+        const bool starved = food <= 0.0;
+        if (starved) food = 0.0;
+        status = starved ? 1 : kill ? 2 : status_old;
+        const bool done = starved || kill || status_old != 0 || h.turn >= p.max_turns;
+        {
+          const double r_finish = sreg(p.r_finish), r_turn = sreg(p.r_turn);
+          const double r_starve = sreg(p.r_starve), r_killed = sreg(p.r_killed);
+          reward += sel_f64(status == 0, sel_f64(done, r_finish, r_turn), sel_f64(status == 1, r_starve, r_killed));
+        }
+        job = done && p.autoreset;
+        __builtin_nontemporal_store((float)reward, p.reward + g);
+        __builtin_nontemporal_store((uint8_t)(done ? 1 : 0), p.done + g);
+        uint8_t* fts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_food_turns, (uint64_t)p.food_turns));
+        uint8_t* rls = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_role, (uint64_t)p.role));
+        uint8_t* sts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_status, (uint64_t)p.status));
+        if (!job || p.t_planes) {
+          fts[g] = (uint8_t)(int)ceil(food * (double)p.turns_empty);  // :450-452
+          rls[g] = (uint8_t)h.role;
+          sts[g] = (uint8_t)status;
+        }
+        if (!h.valid_action) atomicAdd(&p.counters[2], 1ull);
+      }
+      info[lane] = (job ? 1u : 0u) | (emptied ? 2u : 0u);
+      const unsigned long long jm = __ballot(job);
+      if (job) {
+        const int j = __popcll(jm & ((1ull << lane) - 1ull));
+        const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
+        jobEnv[j] = (uint32_t)lane;
+        *reinterpret_cast<uint2*>(&jobKey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
+      }
+      if (lane == 0) {
+        blk[0] = (uint32_t)__popcll(jm);
+        blk[1] = (uint32_t)jm;
+        blk[2] = (uint32_t)(jm >> 32);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      WIDE_STAMP(3);
+      lds_barrier();  // B2: job list, spawn masks
+      WIDE_STAMP(4);
+      // ------------------------------------------------ W0 P2: spawns, state of continuing envs
+      if (active && !job) {
+        if (p.wolves_on) {
+          for (int w = 0; w < (int)((p.R + 31) >> 5); ++w) {
+            uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w];
+            while (bits) {
+              const int b = __ffs(bits) - 1;
+              bits &= bits - 1;
+              const uint32_t t = xy_add(h.cpos, p.tables[p.ring_at + 32 * w + b]);
+              bool placed = false;
+#pragma unroll
+              for (int k = 0; k < SLOTS; ++k)
+                if (!placed && !((live >> k) & 1u)) { wr[k] = t; live |= 1u << k; placed = true; }
+              if (!placed) wolf_of += 1;
+            }
+          }
+        }
+        int n = 0;
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k)
+          if ((live >> k) & 1u) p.wolves[(int64_t)(n++) * p.B + g] = wr[k];
+        p.hdr[g] = make_uint4(h.cpos, (uint32_t)h.turn,
+                              misc_pack((uint32_t)h.role, (uint32_t)status, (uint32_t)n, (uint32_t)ne, (uint32_t)ndep),
+                              h.hdr.w);
+        p.food[g] = food;
+      }
+    } else if (wave == 1) {
+      // ------------------------------------------------ W1 P0: the view bitmap
+      __builtin_amdgcn_s_setprio(2);
+      uint32_t w[32];
+#pragma unroll
+      for (int i = 0; i < 32; ++i) w[i] = 0u;
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+          if (i < p.W) w[i] = p.bushmap[(int64_t)i * p.B + g];
+      }
+      for (int k = lane; k < p.max_berries; k += 64) thr[k] = p.thresholds[k];
+      const uint32_t strip = active ? strip_bits(p, h) : 0u;
+      const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
+      const uint32_t top = 1u << (p.H - 1);
+      // scroll (generate_bushes keeps the tiles in view, :613-629) + the entering strip
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        if (i >= p.W) break;
+        const uint32_t prev = i > 0 ? w[i - 1] : 0u, next = i < 31 ? w[i + 1] : 0u;
+        const uint32_t sb = (strip >> i) & 1u;
+        uint32_t v = w[i];
+        v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
+        v = h.dir == DIR_LEFT ? (i == p.W - 1 ? strip : next) : v;
+        v = h.dir == DIR_UP ? (((w[i] << 1) & hmask) | sb) : v;
+        v = h.dir == DIR_DOWN ? ((w[i] >> 1) | (sb ? top : 0u)) : v;
+        bm[me + (uint32_t)i] = v;
+      }
+      // emptied tiles that scrolled back into view are absent from S (:506): clear every
+      // emptied log tile in view (idempotent for the ones already absent)
+      const int ne1 = (int)misc_ne(h.hdr.z), ndep1 = (int)misc_ndep(h.hdr.z);
+      if (active && ndep1 > 0 && h.dir != DIR_STAY) {
+        for (int i = 0; i < ne1; ++i) {
+          if (p.eaten_rem[(int64_t)i * p.B + g] != 0) continue;
+          const uint32_t t = p.eaten_xy[(int64_t)i * p.B + g];
+          const int ddx = h.ox - xy_x(t), ddy = h.oy - xy_y(t);
+          if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+        }
+      }
+      // the generated berries of the ostrich's tile (:631-635), for W0
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t cv = 0;
+      if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
+        cv = (uint32_t)bush_value(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1));
+      cval[lane] = cv;
+      __builtin_amdgcn_s_setprio(0);
+      WIDE_STAMP(9);
+      lds_barrier();  // B1
+      WIDE_STAMP(10);
+      lds_barrier();  // B2
+      WIDE_STAMP(11);
+    } else {
+      // ------------------------------------------------ W2, W3 P0: wolf grids, spawn ring
+      {
+        u32x4* z = reinterpret_cast<u32x4*>(wp);
+        const u32x4 zero = {0u, 0u, 0u, 0u};
+        for (int i = tid - 128; i < (int)((64u * P + 4u) >> 2); i += 128) z[i] = zero;
+      }
+      if (p.wolves_on) {
+        const int RW = (p.R + 31) >> 5;
+        for (int w = wave - 2; w < RW; w += 2) {
+          const uint32_t bits = active ? ring_word(p, h, w) : 0u;
+          spawn[(uint32_t)lane * L.spw + (uint32_t)w] = bits;
+        }
+      }
+      WIDE_STAMP(8 * wave + 1);
+      lds_barrier();  // B1
+      WIDE_STAMP(8 * wave + 2);
+      lds_barrier();  // B2
+      WIDE_STAMP(8 * wave + 3);
+    }
+  } else {
+    // ------------------------------------------------ MODE_RESET: the flagged envs are jobs
+    if (wave == 0) {
+      job = active && (p.reset_mask == nullptr || p.reset_mask[g] != 0);
+      info[lane] = job ? 1u : 0u;
+      const unsigned long long jm = __ballot(job);
+      if (job) {
+        const int j = __popcll(jm & ((1ull << lane) - 1ull));
+        const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // 0xFFFFFFFF -> episode 0
+        jobEnv[j] = (uint32_t)lane;
+        *reinterpret_cast<uint2*>(&jobKey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
+      }
+      if (lane == 0) {
+        blk[0] = (uint32_t)__popcll(jm);
+        blk[1] = (uint32_t)jm;
+        blk[2] = (uint32_t)(jm >> 32);
+      }
+    }
+    lds_barrier();
+  }
+
+  const int n_jobs = (int)blk[0];
+  const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+  uint8_t* out = p.planes + (size_t)g0 * OB;
+  if constexpr (MODE == MODE_STEP) {
+    // ------------------------------------------------ P2: obs of S, continuing bitmaps
+    uint8_t* tout = p.t_planes ? p.t_planes + (size_t)g0 * OB : nullptr;
+    const uint32_t n = (uint32_t)n_active * CPE;
+    for (uint32_t q = tid; q < n; q += 256) {
+      const uint32_t e = udiv(q, CPE, p.magic_CPE);
+      const bool isjob = (jmask >> e) & 1ull;
+      if (isjob && !tout) continue;
+      const u32x4 v = expand16(chunk_bits(p, bm, wp, e, q - e * CPE));
+      uint8_t* dst = reinterpret_cast<uint8_t*>(sel64(isjob, (uint64_t)tout, (uint64_t)out));
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst) + q);  // streamed: no L2 allocation
+    }
+    for (uint32_t u = tid; u < (uint32_t)p.W * 64u; u += 256) {
+      const uint32_t i = u >> 6, e = u & 63u;
+      if ((int)e >= n_active || ((jmask >> e) & 1ull)) continue;
+      uint32_t v = bm[e * P + i];
+      if ((info[e] & 2u) && i == (uint32_t)p.cw) v &= ~(1u << p.ch);  // eaten empty (post-eat state)
+      p.bushmap[(int64_t)i * p.B + g0 + e] = v;
+    }
+    if (wave == 0) {
+      if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
+      if (lane == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
+    }
+    WIDE_STAMP(8 * wave + 5);
+  } else {
+    if (tid == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
+  }
+
+  if (n_jobs > 0) {
+    // ------------------------------------------------ done envs: new episodes (:231-248)
+    if (MODE == MODE_STEP) lds_barrier();  // B3: the snapshot rows of the jobs are read
+    // reset draws (generate_bushes, initialize_wolves) over the new view, ostrich at (0, 0):
+    // 32 lanes per row, rows written by ballot
+    const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), ts_wolf = make_ts(SITE_SPAWN, 0, 0);
+    const uint32_t rows2 = ((uint32_t)p.W + 1u) >> 1;  // wave-units of two rows
+    for (int jj = 0; jj < n_jobs; ++jj) {
+      const uint32_t e = jobEnv[jj];
+      const uint2 kq = *reinterpret_cast<const uint2*>(&jobKey[2 * jj]);
+      for (uint32_t r2 = (uint32_t)wave; r2 < rows2; r2 += 4u) {
+        const uint32_t i = 2u * r2 + ((uint32_t)lane >> 5), j = (uint32_t)lane & 31u;
+        const bool cell = i < (uint32_t)p.W && j < (uint32_t)p.H;
+        const uint32_t xy = xy_pack(p.cw - (int)i, p.ch - (int)j);
+        const uint32_t h1 = fmix32(xy ^ kq.x);
+        const uint32_t hb = fmix32(h1 ^ ts_bush ^ kq.y);
+        const bool bush = cell && U_ge(h1, hb, ts_bush, kq.x, p.bush_th, p.bush_tl);
+        bool wolf = false;
+        if (p.wolves_on) {
+          const uint32_t hw = fmix32(h1 ^ ts_wolf ^ kq.y);
+          wolf = cell && !U_ge(h1, hw, ts_wolf, kq.x, p.spawn_th, p.spawn_tl);
+        }
+        const unsigned long long bb = __ballot(bush), bw = __ballot(wolf);
+        if ((lane & 31) == 0 && i < (uint32_t)p.W) {
+          bm[e * P + i] = (uint32_t)(lane ? bb >> 32 : bb);
+          wp[e * P + i] = (uint32_t)(lane ? bw >> 32 : bw);
+        }
+      }
+    }
+    lds_barrier();  // B4
+    if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
+      // spawn_ostriches (:595-611) and the initial wolves, one per wolf cell of the view
+      const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
+      const uint32_t kb0 = (uint32_t)ek2, kb1 = (uint32_t)(ek2 >> 32);
+      const double food2 = p.start_food_random
+                               ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
+                               : p.start_food;
+      const int role2 = p.start_role_random
+                            ? (int)(draw_U(xy_pack(0, 0), make_ts(SITE_START_ROLE, 0, 0), kb0, kb1) >> 52)
+                            : p.start_role;
+      int n = 0;
+      for (int i = 0; i < p.W; ++i) {
+        uint32_t bits = wp[me + (uint32_t)i];
+        while (bits) {
+          const int j = __ffs(bits) - 1;
+          bits &= bits - 1;
+          if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = xy_pack(p.cw - i, p.ch - j);
+          else wolf_of += 1;
+        }
+      }
+      p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
+      p.food[g] = food2;
+      p.food_turns[g] = (uint8_t)(int)ceil(food2 * (double)p.turns_empty);
+      p.role[g] = (uint8_t)role2;
+      p.status[g] = 0;
+    }
+    // the new episodes' obs and bitmaps
+    for (int jj = 0; jj < n_jobs; ++jj) {
+      const uint32_t e = jobEnv[jj];
+      for (uint32_t r = tid; r < CPE; r += 256) {
+        const u32x4 v = expand16(chunk_bits(p, bm, wp, e, r));
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out) + e * CPE + r);
+      }
+      for (uint32_t i = tid; i < (uint32_t)p.W; i += 256) p.bushmap[(int64_t)i * p.B + g0 + e] = bm[e * P + i];
+    }
+  }
+  if (wave == 0 && wolf_of) atomicAdd(&p.counters[0], wolf_of);
+}
+
+#define WAB_WIDE_INST(M, S) template __global__ void wab_step_wide<M, S>(Params);
+WAB_WIDE_INST(MODE_STEP, 8)
+WAB_WIDE_INST(MODE_STEP, 16)
+WAB_WIDE_INST(MODE_STEP, 32)
+WAB_WIDE_INST(MODE_RESET, 8)
+WAB_WIDE_INST(MODE_RESET, 16)
+WAB_WIDE_INST(MODE_RESET, 32)
+
+}  // namespace wab

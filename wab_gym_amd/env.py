@@ -183,6 +183,11 @@ class BatchedWolvesAndBushesEnv:
                                           img.data_ptr(), self._stream()), "wab_render")
         return img
 
+    @property
+    def step_kernel(self):
+        """Which fused step kernel this handle launches: "small", "wide" or "block"."""
+        return _lib.load().wab_step_kernel(self._h).decode()
+
     def counters(self):
         c = _lib.WabCounters()
         _lib.check(_lib.load().wab_get_counters(self._h, ctypes.addressof(c), self._stream()),
