@@ -46,9 +46,11 @@ def main():
     L.wab_debug_set_stamps(env._h, st.data_ptr())
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
-    kind = os.environ.get("WAB_STEP_KERNEL", "small")
-    if kind != "block":
+    kind = env.step_kernel
+    if kind == "small":
         return small_report(env, st, g, args.steps)
+    if kind == "wide":
+        return wide_report(env, st, g, args.steps)
     acc, spans, starts, ends, slow_acc = [], [], [], [], []
     sub_acc = {k: [] for k in [(2, 7), (7, 8), (8, 9), (9, 3)]}
     for t in range(args.steps):
@@ -88,6 +90,61 @@ def main():
     for n, a0, a1 in sub:
         v = np.mean(sub_acc[(a0, a1)]) * 10 / 1000
         print("  %-20s %7.2f us" % (n, v))
+
+
+def wide_report(env, st, g, steps):
+    """wab_step_wide: wave w stamps 8w + (0 start, 1 before B1, 2 after B1, 3/4 after its P1
+    parts, 5 after B2, 6 after its stores retired)."""
+    import numpy as np
+    import torch
+
+    B = env.num_envs
+    nb = (B + 63) // 64
+    waves = {"W0 dynamics": ([0, 1, 2, 3, 4, 5, 6], ["loads, despawn, pursuit, grid", "B1 wait", "eat, starve, done",
+                                                    "obs issue", "B2 wait", "P2 + drain"]),
+             "W1 bushes": ([8, 9, 10, 11, 12, 13, 14], ["bitmap loads, strip, value", "B1 wait", "obs issue",
+                                                        "ring B", "B2 wait", "P2 + drain"]),
+             "W2 ring": ([16, 17, 18, 19, 20, 21, 22], ["ring A", "B1 wait", "obs issue", "ring B", "B2 wait",
+                                                      "P2 + drain"]),
+             "W3 ring": ([24, 25, 26, 27, 28, 29, 30], ["ring offsets, ring A", "B1 wait", "obs issue", "ring B",
+                                                      "B2 wait", "P2 + drain"])}
+    acc = {k: [] for k in waves}
+    spans, ends, starts = [], [], []
+    for t in range(steps):
+        st.zero_()
+        env.step(torch.randint(0, env.n_actions, (B,), device="cuda:0", generator=g))
+        torch.cuda.synchronize()
+        if t < 20:
+            continue
+        s = st.cpu().numpy().astype(np.int64)[:nb]
+        t0 = s[:, [0, 8, 16, 24]].min()
+        for k, (cols, _) in waves.items():
+            acc[k].append(np.diff(s[:, cols], axis=1).mean(axis=0))
+        end = s[:, [6, 14, 22, 30]].max(axis=1)
+        spans.append(end.max() - t0)
+        ends.append(np.percentile(end - t0, [0, 50, 100]))
+        starts.append(np.percentile(s[:, 0] - t0, [0, 50, 90, 100]))
+    for k, (cols, names) in waves.items():
+        a = np.mean(acc[k], axis=0) * 10 / 1000
+        print("%s:" % k)
+        for n, v in zip(names, a):
+            print("  %-36s %7.2f us" % (n, v))
+    print("%-24s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
+    print("workgroup start p0/p50/p90/max (us):", np.round(np.mean(starts, axis=0) * 10 / 1000, 2))
+    print("workgroup end times p0/p50/max (us):", np.round(np.mean(ends, axis=0) * 10 / 1000, 2))
+    us = lambda v: np.round(np.asarray(v) * 10 / 1000, 2)  # noqa: E731
+    print("W1 P0 detail: start->strip done %.2f, ->rows written %.2f, ->value done %.2f us" % (
+        us((s[:, 15] - s[:, 8]).mean()), us((s[:, 31] - s[:, 15]).mean()), us((s[:, 9] - s[:, 31]).mean())))
+    e_ = end - t0
+    print("last step: end by blockIdx %% 8:", us([e_[np.arange(nb) % 8 == x].mean() for x in range(8)]))
+    print("last step: end by blockIdx quartile:", us([q.mean() for q in np.array_split(e_, 4)]))
+    obs = s[:, 11] - s[:, 10]
+    print("last step: W1 obs issue p0/p50/p90/max:", us(np.percentile(obs, [0, 50, 90, 100])))
+    print("last step: W1 obs start (from t0) p0/p50/p90/max:", us(np.percentile(s[:, 10] - t0, [0, 50, 90, 100])))
+    order = np.argsort(e_)
+    for name, idx in (("fastest 10%", order[: nb // 10]), ("slowest 10%", order[-nb // 10:])):
+        print("  %s: obs start %.2f, obs issue %.2f, drain %.2f, end %.2f us" % (
+            name, us((s[idx, 10] - t0).mean()), us(obs[idx].mean()), us((s[idx, 14] - s[idx, 13]).mean()), us(e_[idx].mean())))
 
 
 def small_report(env, st, g, steps):

@@ -68,6 +68,7 @@ struct wab_handle {
   uint4* ego_path = nullptr;
   uint32_t* ego_diamond = nullptr;
   int ego_cap = 0, ego_n_diamond = 0;
+  size_t wide_lds_bytes = 0;  // LDS per workgroup of the wide kernel (see wab_create)
 };
 
 namespace {
@@ -176,7 +177,7 @@ int launch(wab_handle* h, const Params& p, hipStream_t stream) {
   if (h->n_blocks == 0) return WAB_OK;
   if (h->step_kernel == KERNEL_WIDE) {
     const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
-    const size_t lds = (size_t)wab::wide_layout(p).total * 4u;
+    const size_t lds = h->wide_lds_bytes;
     switch (h->slots) {
       case 8: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 8>), grid, block, lds, stream, p); break;
       case 16: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 16>), grid, block, lds, stream, p); break;
@@ -362,7 +363,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   rc |= alloc((void**)&p.wolves, B * 4 * (size_t)slots);
   rc |= alloc((void**)&p.eaten_xy, B * 4 * (size_t)cap);
   rc |= alloc((void**)&p.eaten_rem, B * (size_t)cap);
-  rc |= alloc((void**)&p.bushmap, B * 4 * (size_t)(p.WHW > p.W ? p.WHW : p.W));  // (wide: W rows)
+  rc |= alloc((void**)&p.bushmap, B * 4 * (size_t)(p.W <= 32 && p.WHW < 32 ? 32 : p.WHW));  // (wide: 32 per env)
   rc |= alloc((void**)&p.counters, 4 * 8);
   rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   uint64_t* thr = nullptr;
@@ -410,11 +411,18 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
                   kernel_ptr<1, false>(slots)})
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
-  if (h->step_kernel == KERNEL_WIDE)
+  if (h->step_kernel == KERNEL_WIDE) {
+    // WAB_WIDE_LDS_KB (experiments): reserve more LDS per workgroup than needed, which caps
+    // the workgroups a CU can hold and so evens out their distribution over the CUs
+    h->wide_lds_bytes = (size_t)wab::wide_layout(p).total * 4u;
+    h->p.obs_nt = 0;  // plain stores measured faster than non-temporal for this pattern
+    if (const char* nt = std::getenv("WAB_OBS_NT")) h->p.obs_nt = std::atoi(nt);
+    if (const char* kb = std::getenv("WAB_WIDE_LDS_KB"))
+      h->wide_lds_bytes = std::max(h->wide_lds_bytes, (size_t)std::atoi(kb) * 1024u);
     for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots)})
       if (e == hipSuccess)
-        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(wab::wide_layout(p).total * 4u));
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_lds_bytes);
+  }
   if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
     e = hipFuncSetAttribute(small_kernel_ptr(slots), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)h->small_lds_bytes);

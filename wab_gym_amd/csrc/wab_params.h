@@ -60,6 +60,7 @@ struct Params {
   int32_t start_role, start_food_random, start_role_random;
   int32_t max_turns, turns_empty;
   int32_t lookout_only, restrict_view, wolves_on, wolves_can_move, god_mode, autoreset;
+  int32_t obs_nt;           // wide kernel: obs stores non-temporal (1) or plain (0)
   uint32_t mask_rows[2][11];  // restrict_view: 11-bit row masks per role (bit j <=> mask[i][j])
   uint32_t small_masks[3][4]; // W*H <= 128: column 0, column H-1, valid-bit masks of the bitmap
   uint32_t view121[2][4];     // restrict_view at 11x11: the row masks as one 121-bit plane mask
@@ -154,7 +155,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
 // different banks (dwords)
 constexpr uint32_t kWidePitch = 33;
 struct WideLayout {
-  uint32_t bm, wp, spawn, spw, thr, cval, info, blk, jobEnv, jobKey, total;
+  uint32_t bm, wp, spawn, spw, ring, thr, cval, info, blk, jobEnv, jobKey, total;
 };
 
 __host__ __device__ inline WideLayout wide_layout(const Params& p) {
@@ -166,6 +167,7 @@ __host__ __device__ inline WideLayout wide_layout(const Params& p) {
   o = lds_align4(o);
   L.spw = (((uint32_t)p.R + 31u) >> 5) | 1u;  // spawn-mask dwords per env (odd pitch)
   L.spawn = o; o += lds_align4(64u * L.spw);
+  L.ring = o; o += lds_align4((uint32_t)p.R);  // spawn-ring offsets
   L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
   L.cval = o; o += 64u;                       // generated berries of the ostrich's tile
   L.info = o; o += 64u;                       // W0 -> all: job | emptied << 1

@@ -2,27 +2,33 @@
 // S = 16 or 32 bytes, no restrict_view (the 31x31-in-32x32 configuration C3 of SURVEY.md).
 //
 // At 31x31 the step is dominated by its output: 2976 obs bytes per env against ~230 bytes
-// of state, so the kernel is organised around getting the obs stores out early and at full
-// width.  One 256-thread workgroup serves 64 envs; each wave runs one lane per env:
+// of state, so the kernel is organised around getting the obs stores out early, from all
+// four SIMDs, with the remaining hash work overlapping their drain.  One 256-thread
+// workgroup serves 64 envs; each wave runs one lane per env:
 //
-//          W0 dynamics            W1 bushes               W2, W3 ring
-//   P0     state + log loads,     bitmap rows (one dword  zero the wolf grids,
-//          despawn, pursuit,      per row), scroll,       spawn-ring draws
-//          kill                   entering row/column
+//          W0 dynamics            W1 bushes               W2             W3 ring
+//   P0     state + log loads,     bitmap rows (one dword  first spawn-   ring offsets
+//          despawn, pursuit,      per row), scroll,       ring word      -> LDS
+//          kill, wolf grid of S   entering row/column
 //                                 draws, emptied tiles,
 //                                 ostrich-tile value
-//   -- B1 --
-//   P1     wolf grid, eat, hunger, starve, reward/done, scalars, job list
+//   -- B1 --  S (the obs snapshot) is complete
+//   P1     eat, hunger, starve,   obs chunks of S         obs chunks     the rest of
+//          reward/done, scalars,                          of S           the ring
+//          job list; obs chunks
 //   -- B2 --
-//   P2     W0: spawns, state stores; all: obs chunks (16 bytes: one row half of one plane)
-//          of the continuing envs (+ terminal obs), bitmap stores
+//   P2     W0: spawns, state stores; all: post-eat bitmaps, terminal obs of done envs
 //   (done envs: B3, reset draws by ballot, B4, new episodes, their obs and bitmaps)
 //
-// The view bitmaps live in LDS as one dword per row (bit j = column j): the move scrolls
-// them by a row index (x moves) or a shift (y moves), the entering strip is one row word or
-// one bit per row, and an obs chunk is 16 bits of one row expanded to 16 bytes.  Every obs
-// store wave-instruction writes 1 KiB contiguous.  Reset (MODE_RESET) is the done-env path
-// alone, so the bitmap layout stays private to this kernel.
+// Every wave issues its share of the obs stores as soon as S is complete; nothing after
+// that issues a vector load (vmcnt also counts stores: a load would wait for the drain).
+// The obs of a done env is written twice (S, then the new episode's first obs) by the same
+// thread, so the later store wins.  The view bitmaps live in LDS as one dword per row
+// (bit j = column j): the move scrolls them by a row index (x moves) or a shift (y moves),
+// the entering strip is one row word or one bit per row, and an obs chunk is 16 bits of
+// one row expanded to 16 bytes; every store wave-instruction writes 1 KiB contiguous.
+// Reset (MODE_RESET) is the done-env path alone, so the bitmap layout stays private to
+// this kernel: env-major, 32 dwords per env (one 128-byte line; rows past W unused).
 #include <hip/hip_runtime.h>
 
 #include "wab_small.h"
@@ -125,14 +131,16 @@ __device__ __forceinline__ uint32_t strip_bits(const Params& p, const WHead& h) 
   return bits;
 }
 
-// spawn draws (spawn_wolves :527-576, wolf iff u < p/2) of ring tiles [32 w, 32 w + 32)
-__device__ __forceinline__ uint32_t ring_word(const Params& p, const WHead& h, int w) {
+// spawn draws (spawn_wolves :527-576, wolf iff u < p/2) of ring tiles [32 w, 32 w + 32);
+// the ring offsets come from the LDS copy (a scalar load from L2 stalls for microseconds
+// once the obs stores are streaming)
+__device__ __forceinline__ uint32_t ring_word(const Params& p, const WHead& h, const uint32_t* ring_lds, int w) {
   const int r0 = 32 * w, r1 = min(p.R, r0 + 32);
   const uint32_t ts = make_ts(SITE_SPAWN, 0, h.turn), hk = ts ^ h.b1;
-  const uint4* ring = reinterpret_cast<const uint4*>(p.tables + p.ring_at);  // uniform: scalar loads
+  const uint4* ring = reinterpret_cast<const uint4*>(ring_lds);
   uint32_t bits = 0;
   for (int r = r0; r < r1; r += 4) {
-    const uint4 o = ring[r >> 2];  // padded to a multiple of 4 entries
+    const uint4 o = ring[r >> 2];  // padded to a multiple of 4 entries (broadcast read)
     uint32_t h1[4] = {xy_add(h.cpos, o.x) ^ h.b0, xy_add(h.cpos, o.y) ^ h.b0, xy_add(h.cpos, o.z) ^ h.b0,
                       xy_add(h.cpos, o.w) ^ h.b0};
     fmix32x4(h1);
@@ -157,11 +165,25 @@ __device__ __forceinline__ uint32_t ring_word(const Params& p, const WHead& h, i
   return bits;
 }
 
+// dst[i] = src[i] for i < n by one wave, four independent loads per lane in flight at a time
+// (a plain strided loop waits for each load before its LDS store)
+template <typename T>
+__device__ __forceinline__ void copy_to_lds(T* dst, const T* src, int n, int lane) {
+  for (int i0 = 0; i0 < n; i0 += 256) {
+    T v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = src[min(i0 + 64 * k + lane, n - 1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + 64 * k + lane < n) dst[i0 + 64 * k + lane] = v[k];
+  }
+}
+
 // 16 cells of one row -> 16 bytes
 __device__ __forceinline__ u32x4 expand16(uint32_t v) {
   u32x4 q;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) q[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+  for (int k = 0; k < 4; ++k) q[k] = __umul24((v >> (4 * k)) & 0xFu, 0x00204081u) & 0x01010101u;
   return q;
 }
 
@@ -179,6 +201,63 @@ __device__ __forceinline__ uint32_t chunk_bits(const Params& p, const uint32_t* 
   return (row >> (16u * half)) & 0xFFFFu;
 }
 
+// Obs chunks (16 bytes).  The ostrich grid (plane 2) is the same in every observation (the
+// centre cell), so W3 writes it while the snapshot S is still being built (obs_plane2); the
+// wolf and bush grids (planes 0, 1) of S follow from the threads of waves 0-2 (obs_main).
+// Chunk r < 2*W*S/16 of env e is always written by thread (e * 2WC + r) % kObsThreads, also
+// when a done env's new-episode obs later overwrites it (obs_env), so both stores come from
+// one thread in program order.
+constexpr uint32_t kObsThreads = 192;
+
+__device__ __forceinline__ void store16(const Params& p, uint8_t* out, uint32_t q, const u32x4& v) {
+  if (p.obs_nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out) + q);
+  else reinterpret_cast<u32x4*>(out)[q] = v;
+}
+
+__device__ __forceinline__ void obs_plane2(const Params& p, uint8_t* out, uint32_t n_active, int lane) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, WC = (uint32_t)p.W * CPR;
+  const uint32_t n = n_active * WC;
+  uint32_t e = 0, r = (uint32_t)lane;
+  while (r >= WC) { r -= WC; ++e; }
+  for (uint32_t c = (uint32_t)lane; c < n; c += 64u) {
+    const uint32_t i = CPR == 2u ? r >> 1 : r, half = CPR == 2u ? r & 1u : 0u;
+    const uint32_t row = i == (uint32_t)p.cw ? 1u << p.ch : 0u;
+    store16(p, out, e * CPE + 2u * WC + r, expand16((row >> (16u * half)) & 0xFFFFu));
+    r += 64u;
+    while (r >= WC) { r -= WC; ++e; }
+  }
+}
+
+__device__ __forceinline__ void obs_main(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                         uint32_t n_active, int tid) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4, C2 = 2u * (((uint32_t)p.S >> 4) * (uint32_t)p.W);
+  const uint32_t n = n_active * C2;
+  uint32_t e = 0, r = (uint32_t)tid;
+  while (r >= C2) { r -= C2; ++e; }
+  for (uint32_t c = (uint32_t)tid; c < n; c += kObsThreads) {
+    store16(p, out, e * CPE + r, expand16(chunk_bits(p, bm, wp, e, r)));
+    r += kObsThreads;
+    while (r >= C2) { r -= C2; ++e; }
+  }
+}
+
+// planes 0, 1 of one env, same thread mapping as obs_main (threads >= kObsThreads idle)
+__device__ __forceinline__ void obs_env(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                        uint32_t e, int tid) {
+  if ((uint32_t)tid >= kObsThreads) return;
+  const uint32_t CPE = (uint32_t)p.OB >> 4, C2 = 2u * (((uint32_t)p.S >> 4) * (uint32_t)p.W);
+  const uint32_t base = e * C2;
+  for (uint32_t r = ((uint32_t)tid + kObsThreads - base % kObsThreads) % kObsThreads; r < C2; r += kObsThreads)
+    store16(p, out, e * CPE + r, expand16(chunk_bits(p, bm, wp, e, r)));
+}
+
+// all three planes of one env (terminal observations)
+__device__ __forceinline__ void obs_env_all(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                            uint32_t e, int tid) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4;
+  for (uint32_t r = (uint32_t)tid; r < CPE; r += 256u) store16(p, out, e * CPE + r, expand16(chunk_bits(p, bm, wp, e, r)));
+}
+
 }  // namespace
 
 template <int MODE, int SLOTS>
@@ -194,6 +273,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   uint32_t* bm = lds + L.bm;
   uint32_t* wp = lds + L.wp;
   uint32_t* spawn = lds + L.spawn;
+  uint32_t* ring = lds + L.ring;
   uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr);
   uint32_t* cval = lds + L.cval;
   uint32_t* info = lds + L.info;
@@ -201,8 +281,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   uint32_t* jobEnv = lds + L.jobEnv;
   uint32_t* jobKey = lds + L.jobKey;
   constexpr uint32_t P = kWidePitch;
-  const uint32_t OB = (uint32_t)p.OB, CPE = OB >> 4;
+  const uint32_t OB = (uint32_t)p.OB;
   const uint32_t me = (uint32_t)lane * P;
+  uint8_t* out = p.planes + (size_t)g0 * OB;
+  const int RW = (p.R + 31) >> 5;                 // spawn-ring words
+  const int nA = p.wolves_on ? min(RW, 1) : 0;    // words drawn before B1 (W2); the rest: W3 after B1
 
   const WHead h = whead<MODE>(p, g, active);
 
@@ -218,8 +301,9 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
 
   if constexpr (MODE == MODE_STEP) {
     WIDE_STAMP(8 * wave);
+
     if (wave == 0) {
-      // ------------------------------------------------ W0 P0: loads, despawn, pursuit, kill
+      // ------------------------------------------------ W0 P0: loads, despawn, pursuit, kill, wolf grid
       __builtin_amdgcn_s_setprio(3);  // the longest chain
       uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
       if (active) {
@@ -233,6 +317,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
             lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
           }
       }
+      for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;  // (while the loads are in flight)
       const int nw = (int)misc_nw(h.hdr.z);
       ne = (int)misc_ne(h.hdr.z);
       ndep = (int)misc_ndep(h.hdr.z);
@@ -278,7 +363,8 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         }
         live = keep;
       }
-      // pursuit (:267-286): one axis step toward the ostrich, ties along x; kill (:291-297)
+      // pursuit (:267-286): one axis step toward the ostrich, ties along x; the wolf grid of S
+      // (:412-428); kill (:291-297)
       bool kill = false;
 #pragma unroll
       for (int k = 0; k < SLOTS; ++k) {
@@ -291,7 +377,9 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
           wy += alongx ? 0 : sgn(ddy);
           wr[k] = xy_pack(wx, wy);
         }
-        kill |= wx == h.ox && wy == h.oy;
+        const int ddx = h.ox - wx, ddy = h.oy - wy;
+        if (active && abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
+        kill |= ddx == 0 && ddy == 0;
       }
       kill = kill && !p.god_mode;
       // eaten log, first entries: the ostrich's tile
@@ -300,17 +388,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       for (int k = 0; k < 4; ++k)
         if (k < ne && lxy[k] == h.cpos) { found = k; found_rem = (int)lrem[k]; }
       WIDE_STAMP(1);
-      lds_barrier();  // B1: bitmap rows, the ostrich-tile value, zeroed wolf grids
+      lds_barrier();  // B1: S complete (bitmap rows, wolf grids); the ostrich-tile value
       WIDE_STAMP(2);
-      // ------------------------------------------------ W0 P1: grid of S, eat, starve, done
+      // ------------------------------------------------ W0 P1: eat, starve, done; then obs
       double reward = 0.0;
       if (active) {
-#pragma unroll
-        for (int k = 0; k < SLOTS; ++k) {  // wolf grid (:412-428), snapshot #2
-          if (!((live >> k) & 1u)) continue;
-          const int ddx = h.ox - xy_x(wr[k]), ddy = h.oy - xy_y(wr[k]);
-          if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
-        }
         const bool center_bush = ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u) != 0u;
         if (center_bush && found < 0 && ne > 4) {
           for (int i = 4; i < ne; ++i)
@@ -375,17 +457,19 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       }
       __builtin_amdgcn_s_setprio(0);
       WIDE_STAMP(3);
-      lds_barrier();  // B2: job list, spawn masks
+      obs_main(p, bm, wp, out, (uint32_t)n_active, tid);
       WIDE_STAMP(4);
+      lds_barrier();  // B2: job list, spawn masks
+      WIDE_STAMP(5);
       // ------------------------------------------------ W0 P2: spawns, state of continuing envs
       if (active && !job) {
         if (p.wolves_on) {
-          for (int w = 0; w < (int)((p.R + 31) >> 5); ++w) {
+          for (int w = 0; w < RW; ++w) {
             uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w];
             while (bits) {
               const int b = __ffs(bits) - 1;
               bits &= bits - 1;
-              const uint32_t t = xy_add(h.cpos, p.tables[p.ring_at + 32 * w + b]);
+              const uint32_t t = xy_add(h.cpos, ring[32 * w + b]);
               bool placed = false;
 #pragma unroll
               for (int k = 0; k < SLOTS; ++k)
@@ -403,77 +487,110 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
                               h.hdr.w);
         p.food[g] = food;
       }
-    } else if (wave == 1) {
-      // ------------------------------------------------ W1 P0: the view bitmap
-      __builtin_amdgcn_s_setprio(2);
-      uint32_t w[32];
-#pragma unroll
-      for (int i = 0; i < 32; ++i) w[i] = 0u;
-      if (active) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i)
-          if (i < p.W) w[i] = p.bushmap[(int64_t)i * p.B + g];
-      }
-      for (int k = lane; k < p.max_berries; k += 64) thr[k] = p.thresholds[k];
-      const uint32_t strip = active ? strip_bits(p, h) : 0u;
-      const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
-      const uint32_t top = 1u << (p.H - 1);
-      // scroll (generate_bushes keeps the tiles in view, :613-629) + the entering strip
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        if (i >= p.W) break;
-        const uint32_t prev = i > 0 ? w[i - 1] : 0u, next = i < 31 ? w[i + 1] : 0u;
-        const uint32_t sb = (strip >> i) & 1u;
-        uint32_t v = w[i];
-        v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
-        v = h.dir == DIR_LEFT ? (i == p.W - 1 ? strip : next) : v;
-        v = h.dir == DIR_UP ? (((w[i] << 1) & hmask) | sb) : v;
-        v = h.dir == DIR_DOWN ? ((w[i] >> 1) | (sb ? top : 0u)) : v;
-        bm[me + (uint32_t)i] = v;
-      }
-      // emptied tiles that scrolled back into view are absent from S (:506): clear every
-      // emptied log tile in view (idempotent for the ones already absent)
-      const int ne1 = (int)misc_ne(h.hdr.z), ndep1 = (int)misc_ndep(h.hdr.z);
-      if (active && ndep1 > 0 && h.dir != DIR_STAY) {
-        for (int i = 0; i < ne1; ++i) {
-          if (p.eaten_rem[(int64_t)i * p.B + g] != 0) continue;
-          const uint32_t t = p.eaten_xy[(int64_t)i * p.B + g];
-          const int ddx = h.ox - xy_x(t), ddy = h.oy - xy_y(t);
-          if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
-        }
-      }
-      // the generated berries of the ostrich's tile (:631-635), for W0
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      uint32_t cv = 0;
-      if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
-        cv = (uint32_t)bush_value(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1));
-      cval[lane] = cv;
-      __builtin_amdgcn_s_setprio(0);
-      WIDE_STAMP(9);
-      lds_barrier();  // B1
-      WIDE_STAMP(10);
-      lds_barrier();  // B2
-      WIDE_STAMP(11);
     } else {
-      // ------------------------------------------------ W2, W3 P0: wolf grids, spawn ring
-      {
-        u32x4* z = reinterpret_cast<u32x4*>(wp);
-        const u32x4 zero = {0u, 0u, 0u, 0u};
-        for (int i = tid - 128; i < (int)((64u * P + 4u) >> 2); i += 128) z[i] = zero;
-      }
-      if (p.wolves_on) {
-        const int RW = (p.R + 31) >> 5;
-        for (int w = wave - 2; w < RW; w += 2) {
-          const uint32_t bits = active ? ring_word(p, h, w) : 0u;
-          spawn[(uint32_t)lane * L.spw + (uint32_t)w] = bits;
+      if (wave == 1) {
+        // ---------------------------------------------- W1 P0: the view bitmap
+        __builtin_amdgcn_s_setprio(2);
+        // every load up front (vmcnt retires in order; a copy loop would wait for each load
+        // before issuing the next): thresholds, the first eaten-log entries (speculatively),
+        // the bitmap rows (env-major: 32 dwords per env, eight 16-byte loads)
+        const int nthr = p.max_berries;
+        uint64_t tv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
+        const int64_t ga = active ? g : 0;
+        uint32_t ex[4], er[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t row = min(k, p.eaten_cap - 1);
+          ex[k] = p.eaten_xy[row * p.B + ga];
+          er[k] = p.eaten_rem[row * p.B + ga];
+        }
+        uint32_t w[32];
+        {
+          const uint4* src = reinterpret_cast<const uint4*>(p.bushmap + (size_t)ga * 32u);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint4 v = src[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+          }
+        }
+        const uint32_t strip = active ? strip_bits(p, h) : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
+        WIDE_STAMP(15);
+        const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
+        const uint32_t top = 1u << (p.H - 1);
+        // scroll (generate_bushes keeps the tiles in view, :613-629) + the entering strip
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          if (i >= p.W) break;
+          const uint32_t wi = active ? w[i] : 0u;
+          const uint32_t prev = (active && i > 0) ? w[i - 1] : 0u;
+          const uint32_t next = (active && i < 31 && i + 1 < p.W) ? w[i + 1] : 0u;
+          const uint32_t sb = (strip >> i) & 1u;
+          uint32_t v = wi;
+          v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
+          v = h.dir == DIR_LEFT ? (i == p.W - 1 ? strip : next) : v;
+          v = h.dir == DIR_UP ? (((wi << 1) & hmask) | sb) : v;
+          v = h.dir == DIR_DOWN ? ((wi >> 1) | (sb ? top : 0u)) : v;
+          bm[me + (uint32_t)i] = v;
+        }
+        WIDE_STAMP(31);
+        // emptied tiles that scrolled back into view are absent from S (:506): clear every
+        // emptied log tile in view (idempotent for the ones already absent)
+        const int ne1 = (int)misc_ne(h.hdr.z), ndep1 = (int)misc_ndep(h.hdr.z);
+        if (active && ndep1 > 0 && h.dir != DIR_STAY) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int ddx = h.ox - xy_x(ex[k]), ddy = h.oy - xy_y(ex[k]);
+            if (k < ne1 && er[k] == 0u && abs(ddx) <= p.cw && abs(ddy) <= p.ch)
+              bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+          }
+          for (int i = 4; i < ne1; ++i) {  // (rare: more than 4 eaten tiles this episode)
+            if (p.eaten_rem[(int64_t)i * p.B + g] != 0) continue;
+            const uint32_t t = p.eaten_xy[(int64_t)i * p.B + g];
+            const int ddx = h.ox - xy_x(t), ddy = h.oy - xy_y(t);
+            if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+          }
+        }
+        // the generated berries of the ostrich's tile (:631-635), for W0
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t cv = 0;
+        if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
+          cv = (uint32_t)bush_value(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1));
+        cval[lane] = cv;
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+        // ---------------------------------------------- W3 P0: the ostrich grids; W2 P0: ring
+        // offsets -> LDS, first ring word
+        if (wave == 3) obs_plane2(p, out, (uint32_t)n_active, lane);
+        if (wave == 2) {
+          copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          for (int w = 0; w < nA; ++w)
+            spawn[(uint32_t)lane * L.spw + (uint32_t)w] = active ? ring_word(p, h, ring, w) : 0u;
         }
       }
       WIDE_STAMP(8 * wave + 1);
       lds_barrier();  // B1
       WIDE_STAMP(8 * wave + 2);
-      lds_barrier();  // B2
+      // ------------------------------------------------ P1: W1, W2 obs of S; W3 the rest of the
+      // ring (its VALU work on its own SIMD overlaps the drain of the stores)
+      if (wave < 3) obs_main(p, bm, wp, out, (uint32_t)n_active, tid);
       WIDE_STAMP(8 * wave + 3);
+      if (wave == 3 && p.wolves_on)
+        for (int w = nA; w < RW; ++w)
+          spawn[(uint32_t)lane * L.spw + (uint32_t)w] = active ? ring_word(p, h, ring, w) : 0u;
+      WIDE_STAMP(8 * wave + 4);
+      lds_barrier();  // B2
+      WIDE_STAMP(8 * wave + 5);
     }
   } else {
     // ------------------------------------------------ MODE_RESET: the flagged envs are jobs
@@ -498,31 +615,23 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
 
   const int n_jobs = (int)blk[0];
   const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
-  uint8_t* out = p.planes + (size_t)g0 * OB;
   if constexpr (MODE == MODE_STEP) {
-    // ------------------------------------------------ P2: obs of S, continuing bitmaps
-    uint8_t* tout = p.t_planes ? p.t_planes + (size_t)g0 * OB : nullptr;
-    const uint32_t n = (uint32_t)n_active * CPE;
-    for (uint32_t q = tid; q < n; q += 256) {
-      const uint32_t e = udiv(q, CPE, p.magic_CPE);
-      const bool isjob = (jmask >> e) & 1ull;
-      if (isjob && !tout) continue;
-      const u32x4 v = expand16(chunk_bits(p, bm, wp, e, q - e * CPE));
-      uint8_t* dst = reinterpret_cast<uint8_t*>(sel64(isjob, (uint64_t)tout, (uint64_t)out));
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst) + q);  // streamed: no L2 allocation
-    }
-    for (uint32_t u = tid; u < (uint32_t)p.W * 64u; u += 256) {
-      const uint32_t i = u >> 6, e = u & 63u;
-      if ((int)e >= n_active || ((jmask >> e) & 1ull)) continue;
+    // ------------------------------------------------ P2: bitmaps of the continuing envs (post-eat)
+    for (uint32_t u = tid; u < 64u * 32u; u += 256) {  // env-major rows: 128 contiguous bytes per env
+      const uint32_t e = u >> 5, i = u & 31u;
+      if ((int)e >= n_active || ((jmask >> e) & 1ull) || i >= (uint32_t)p.W) continue;
       uint32_t v = bm[e * P + i];
-      if ((info[e] & 2u) && i == (uint32_t)p.cw) v &= ~(1u << p.ch);  // eaten empty (post-eat state)
-      p.bushmap[(int64_t)i * p.B + g0 + e] = v;
+      if ((info[e] & 2u) && i == (uint32_t)p.cw) v &= ~(1u << p.ch);  // eaten empty
+      p.bushmap[(size_t)(g0 + e) * 32u + i] = v;
+    }
+    if (p.t_planes) {  // terminal obs: the step's own obs of every done env
+      uint8_t* tout = p.t_planes + (size_t)g0 * OB;
+      for (unsigned long long jj = jmask; jj; jj &= jj - 1) obs_env_all(p, bm, wp, tout, (uint32_t)(__ffsll(jj) - 1), tid);
     }
     if (wave == 0) {
       if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
       if (lane == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
     }
-    WIDE_STAMP(8 * wave + 5);
   } else {
     if (tid == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
   }
@@ -583,17 +692,19 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       p.role[g] = (uint8_t)role2;
       p.status[g] = 0;
     }
-    // the new episodes' obs and bitmaps
+    // the new episodes' obs (same threads as their S chunks: ordered after them) and bitmaps
     for (int jj = 0; jj < n_jobs; ++jj) {
       const uint32_t e = jobEnv[jj];
-      for (uint32_t r = tid; r < CPE; r += 256) {
-        const u32x4 v = expand16(chunk_bits(p, bm, wp, e, r));
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out) + e * CPE + r);
-      }
-      for (uint32_t i = tid; i < (uint32_t)p.W; i += 256) p.bushmap[(int64_t)i * p.B + g0 + e] = bm[e * P + i];
+      if (MODE == MODE_STEP) obs_env(p, bm, wp, out, e, tid);  // (plane 2 is already right)
+      else obs_env_all(p, bm, wp, out, e, tid);
+      for (uint32_t i = tid; i < (uint32_t)p.W; i += 256) p.bushmap[(size_t)(g0 + e) * 32u + i] = bm[e * P + i];
     }
   }
   if (wave == 0 && wolf_of) atomicAdd(&p.counters[0], wolf_of);
+#ifdef WAB_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  WIDE_STAMP(8 * wave + 6);
+#endif
 }
 
 #define WAB_WIDE_INST(M, S) template __global__ void wab_step_wide<M, S>(Params);
