@@ -20,8 +20,9 @@ __global__ __launch_bounds__(256) void wr(u32x4* out, unsigned per_block, unsign
   }
 }
 
-int main() {
-  const size_t total = 194ull << 20;  // ~ the 31x31 obs of 65536 envs
+int main(int argc, char** argv) {
+  // default ~ the 31x31 obs of 65536 envs; argv[1] = MiB (28 ~ the 11x11 obs)
+  const size_t total = (size_t)(argc > 1 ? atoi(argv[1]) : 194) << 20;
   u32x4* buf;
   hipMalloc(&buf, total + (64 << 20));
   hipEvent_t a, b;

@@ -21,11 +21,16 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--config", default="default")
+    ap.add_argument("--build-only", action="store_true", help="build the stamps library and exit (CPU side)")
+    ap.add_argument("--no-build", action="store_true", help="use the prebuilt stamps library (GPU box)")
     args = ap.parse_args()
     import __graft_entry__ as ge
 
-    src = [os.path.join(ge.CSRC, s) for s in ge.HIP_SOURCES]
-    subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS", "-o", OUT] + src, check=True)
+    if not args.no_build:
+        src = [os.path.join(ge.CSRC, s) for s in ge.HIP_SOURCES]
+        subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS", "-o", OUT] + src, check=True)
+    if args.build_only:
+        return
     os.environ["WAB_LIB"] = OUT
     import numpy as np
     import torch

@@ -19,7 +19,7 @@
 namespace wab {
 template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
-template <int SLOTS>
+template <int SLOTS, int G>
 __global__ void wab_step_small(Params p);
 template <int MODE, int SLOTS>
 __global__ void wab_step_wide(Params p);
@@ -68,6 +68,7 @@ struct wab_handle {
   uint4* ego_path = nullptr;
   uint32_t* ego_diamond = nullptr;
   int ego_cap = 0, ego_n_diamond = 0;
+  bool small_g11 = false;    // the small kernel's 11x11 specialisation (geometry_11)
   size_t wide_lds_bytes = 0;  // LDS per workgroup of the wide kernel (see wab_create)
 };
 
@@ -150,6 +151,10 @@ bool small_view(const Params& p) {
   return p.WH <= 128 && p.S == p.H && p.R <= 128 && (!p.restrict_view || (p.W == 11 && p.H == 11));
 }
 
+// the default options' geometry (11x11 in 11-byte rows, a 48-tile spawn ring): the small
+// kernel's compile-time specialisation G = 11
+bool geometry_11(const Params& p) { return p.W == 11 && p.H == 11 && p.S == 11 && p.margin == 1; }
+
 bool wide_view(const Params& p) {
   return !small_view(p) && p.W <= 32 && p.H <= 32 && (p.S == 16 || p.S == 32) && p.S >= p.H &&
          !p.restrict_view && wab::wide_layout(p).total * 4u <= 64u * 1024u;
@@ -164,11 +169,22 @@ void* wide_kernel_ptr(int slots) {
   }
 }
 
+template <int G>
 void* small_kernel_ptr(int slots) {
   switch (slots) {
-    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8>);
-    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16>);
-    default: return reinterpret_cast<void*>(&wab::wab_step_small<32>);
+    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8, G>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16, G>);
+    default: return reinterpret_cast<void*>(&wab::wab_step_small<32, G>);
+  }
+}
+
+template <int G>
+void launch_small(wab_handle* h, const Params& p, hipStream_t stream) {
+  const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
+  switch (h->slots) {
+    case 8: hipLaunchKernelGGL((wab::wab_step_small<8, G>), grid, block, h->small_lds_bytes, stream, p); break;
+    case 16: hipLaunchKernelGGL((wab::wab_step_small<16, G>), grid, block, h->small_lds_bytes, stream, p); break;
+    default: hipLaunchKernelGGL((wab::wab_step_small<32, G>), grid, block, h->small_lds_bytes, stream, p); break;
   }
 }
 
@@ -184,12 +200,8 @@ int launch(wab_handle* h, const Params& p, hipStream_t stream) {
       default: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 32>), grid, block, lds, stream, p); break;
     }
   } else if (MODE == 0 && h->step_kernel == KERNEL_SMALL) {
-    const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
-    switch (h->slots) {
-      case 8: hipLaunchKernelGGL(wab::wab_step_small<8>, grid, block, h->small_lds_bytes, stream, p); break;
-      case 16: hipLaunchKernelGGL(wab::wab_step_small<16>, grid, block, h->small_lds_bytes, stream, p); break;
-      default: hipLaunchKernelGGL(wab::wab_step_small<32>, grid, block, h->small_lds_bytes, stream, p); break;
-    }
+    if (h->small_g11) launch_small<11>(h, p, stream);
+    else launch_small<0>(h, p, stream);
   } else if (small_map(p)) launch_as<MODE, true>(h, p, stream);
   else launch_as<MODE, false>(h, p, stream);
   HIP_TRY(hipGetLastError());
@@ -342,6 +354,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     const bool forced_block = k && std::strcmp(k, "block") == 0;
     h->step_kernel = forced_block ? KERNEL_BLOCK : small_view(p) ? KERNEL_SMALL : wide_view(p) ? KERNEL_WIDE : KERNEL_BLOCK;
     h->small_lds_bytes = (size_t)wab::small_layout(p).total * 4u;
+    const char* g = std::getenv("WAB_SMALL_GENERIC");  // A/B: the runtime-geometry build
+    h->small_g11 = geometry_11(p) && !(g && std::atoi(g));
   }
   if (h->lds_bytes > 160u * 1024u) {
     delete h;
@@ -424,8 +438,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_lds_bytes);
   }
   if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
-    e = hipFuncSetAttribute(small_kernel_ptr(slots), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)h->small_lds_bytes);
+    e = hipFuncSetAttribute(h->small_g11 ? small_kernel_ptr<11>(slots) : small_kernel_ptr<0>(slots),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->small_lds_bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     std::string msg = std::string("wab_create: ") + hipGetErrorString(e);

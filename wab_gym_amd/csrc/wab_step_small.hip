@@ -100,13 +100,45 @@ __device__ __forceinline__ bool env_done(const Params& p, const Head& h, bool st
   return starved || killed || misc_status(h.hdr.z) != 0 || h.turn >= p.max_turns;
 }
 
+// Geometry specialisation.  G = 11 is the default options' geometry (11x11 view in 11-byte
+// rows, wolf_spawn_margin 1: a 48-tile ring); G = 0 reads everything from the parameter block.
+// With G = 11 the geometry fields are compile-time constants (specialise_geometry) and the ring
+// offsets are immediates instead of scalar loads from the tile table (each a wait on the scalar
+// cache inside the ring loop); fewer live uniform values also cut the SGPR spills.
+template <int G>
+__device__ __forceinline__ void specialise_geometry(Params& p) {
+  if constexpr (G == 11) {
+    p.W = 11; p.H = 11; p.S = 11; p.cw = 5; p.ch = 5; p.margin = 1;
+    p.OB = 363; p.WH = 121; p.R = 48; p.NT = 169; p.RW = 2; p.WHW = 4; p.SL = 11;
+    p.ring_at = 124;
+    p.small_masks[0][0] = 0x00400801u; p.small_masks[0][1] = 0x00801002u;  // column 0 (j = 0)
+    p.small_masks[0][2] = 0x01002004u; p.small_masks[0][3] = 0x00004008u;
+    p.small_masks[1][0] = 0x00200400u; p.small_masks[1][1] = 0x00400801u;  // column H-1
+    p.small_masks[1][2] = 0x00801002u; p.small_masks[1][3] = 0x01002004u;
+    p.small_masks[2][0] = ~0u; p.small_masks[2][1] = ~0u; p.small_masks[2][2] = ~0u;
+    p.small_masks[2][3] = (1u << 25) - 1u;
+  }
+}
+
+// spawn-ring tile r of the G = 11 geometry: the host's table order (wab_create), the 13-wide
+// bands y = 0 and y = 12 first, then the x = 0 / x = 12 columns of rows 1..11
+__host__ __device__ constexpr uint32_t ring11(int r) {
+  const int xi = r < 26 ? r % 13 : ((r - 26) / 11 < 1 ? 0 : 12);
+  const int yi = r < 26 ? (r / 13 < 1 ? 0 : 12) : 1 + (r - 26) % 11;
+  return ((uint32_t)(xi - 6) & 0xFFFFu) | ((uint32_t)(yi - 6) << 16);
+}
+
 // spawn draws (spawn_wolves :527-576, wolf iff u < p/2) on ring tiles [r0, r1), r0 % 4 == 0
+template <int G>
 __device__ __forceinline__ void ring_part(const Params& p, const Head& h, uint32_t b0, uint32_t b1, int r0, int r1,
                                           M128& spawn) {
   const uint32_t ts = make_ts(SITE_SPAWN, 0, h.turn), hk = ts ^ b1;
   const uint4* ring = reinterpret_cast<const uint4*>(p.tables + p.ring_at);  // uniform: scalar loads
+  constexpr int kUnroll = G == 11 ? 16 : 1;
+#pragma unroll kUnroll
   for (int r = r0; r < r1; r += 4) {
-    const uint4 o = ring[r >> 2];  // padded to a multiple of 4 entries
+    // padded to a multiple of 4 entries
+    const uint4 o = G == 11 ? make_uint4(ring11(r), ring11(r + 1), ring11(r + 2), ring11(r + 3)) : ring[r >> 2];
     uint32_t h1[4] = {xy_add(h.cpos, o.x) ^ b0, xy_add(h.cpos, o.y) ^ b0, xy_add(h.cpos, o.z) ^ b0,
                       xy_add(h.cpos, o.w) ^ b0};
     fmix32x4(h1);
@@ -317,7 +349,7 @@ __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const
 }
 
 // --------------------------------------------------------------------------- W0: bushes
-template <int SLOTS>
+template <int SLOTS, int G>
 __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g0 = (int64_t)blockIdx.x * 64;
@@ -444,7 +476,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
   {  // spawn ring part W0 (the helpers' parts are longer: they start it earlier)
     M128 spawn = {0ull, 0ull};
-    if (p.wolves_on) ring_part(p, h, b0, b1, 0, ring_cut(p, 2), spawn);
+    if (p.wolves_on) ring_part<G>(p, h, b0, b1, 0, ring_cut(p, 2), spawn);
     s.spawn[192 + lane] = m_pack(spawn);
   }
   SMALL_STAMP(3);
@@ -514,6 +546,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
 }
 
 // --------------------------------------------------------------------------- W1: draws
+template <int G>
 __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
@@ -533,7 +566,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   SMALL_STAMP(11);
   // spawn ring part W1
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part(p, h, b0, b1, ring_cut(p, 2), ring_cut(p, 4), spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 2), ring_cut(p, 4), spawn);
   s.spawn[lane] = m_pack(spawn);
   SMALL_STAMP(12);
   lds_barrier();  // B1
@@ -576,7 +609,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
 }
 
 // --------------------------------------------------------------------------- W2: wolves
-template <int SLOTS>
+template <int SLOTS, int G>
 __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
@@ -665,7 +698,7 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   SMALL_STAMP(17);
   // ring part B
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part(p, h, b0, b1, ring_cut(p, 4), ring_cut(p, 7), spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 4), ring_cut(p, 7), spawn);
   s.spawn[64 + lane] = m_pack(spawn);
   SMALL_STAMP(18);
   lds_barrier();  // B1: every ring part, the starve flags and the bushes' counts are in
@@ -681,7 +714,8 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
       while (bits) {
         const int b = __ffsll((unsigned long long)bits) - 1;
         bits &= bits - 1;
-        const uint32_t w = xy_add(h.cpos, p.tables[p.ring_at + 64 * half + b]);
+        const int r = 64 * half + b;
+        const uint32_t w = xy_add(h.cpos, G == 11 ? ring11(r) : p.tables[p.ring_at + r]);
         bool placed = false;
 #pragma unroll
         for (int k = 0; k < SLOTS; ++k)
@@ -713,7 +747,7 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
 }
 
 // --------------------------------------------------------------------------- W3: ring
-template <int SLOTS>
+template <int SLOTS, int G>
 __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
@@ -729,7 +763,7 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
   // ring part C
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part(p, h, b0, b1, ring_cut(p, 7), p.R, spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 7), p.R, spawn);
   s.spawn[128 + lane] = m_pack(spawn);
   SMALL_STAMP(23);
   lds_barrier();  // B1
@@ -795,8 +829,10 @@ __device__ __forceinline__ void store_obs(const Params& p, const uint32_t* strea
 
 }  // namespace
 
-template <int SLOTS>
-__global__ __launch_bounds__(256) void wab_step_small(Params p) {
+template <int SLOTS, int G>
+__global__ __launch_bounds__(256) void wab_step_small(Params p0) {
+  Params p = p0;
+  specialise_geometry<G>(p);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const SmallLayout L = small_layout(p);
   if ((int64_t)blockIdx.x * 64 >= p.B) return;  // (uniform over the workgroup)
@@ -805,18 +841,21 @@ __global__ __launch_bounds__(256) void wab_step_small(Params p) {
     // the bushes wave carries the longest chain and shares its SIMD with three helper waves
     // of other groups: let the arbiter issue its instructions first
     __builtin_amdgcn_s_setprio(3);
-    bushes_wave<SLOTS>(p, L, lds, lane);
+    bushes_wave<SLOTS, G>(p, L, lds, lane);
     __builtin_amdgcn_s_setprio(0);
   }
   else if (wave == 1)
-    draws_wave(p, L, lds, lane);
-  else if (wave == 2) wolves_wave<SLOTS>(p, L, lds, lane);
-  else ring_wave<SLOTS>(p, L, lds, lane);
+    draws_wave<G>(p, L, lds, lane);
+  else if (wave == 2) wolves_wave<SLOTS, G>(p, L, lds, lane);
+  else ring_wave<SLOTS, G>(p, L, lds, lane);
   store_obs(p, lds + L.stream, threadIdx.x);
 }
 
-template __global__ void wab_step_small<8>(Params);
-template __global__ void wab_step_small<16>(Params);
-template __global__ void wab_step_small<32>(Params);
+template __global__ void wab_step_small<8, 0>(Params);
+template __global__ void wab_step_small<16, 0>(Params);
+template __global__ void wab_step_small<32, 0>(Params);
+template __global__ void wab_step_small<8, 11>(Params);
+template __global__ void wab_step_small<16, 11>(Params);
+template __global__ void wab_step_small<32, 11>(Params);
 
 }  // namespace wab
