@@ -1,6 +1,6 @@
 """Benchmark: batched Wolves-and-Bushes env-steps/s on MI355X (BASELINE.json `metric`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config default|wide31]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config default|wide31|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A step = one fused-kernel pass (wab_step) over all B envs of a rank: move, wolves, bushes,
@@ -31,7 +31,13 @@ CONFIGS = {
     # 16 wolf slots: with 8, a 961-cell reset view overflows a few times per million resets
     "wide31": ({"width": 31, "height": 31}, 32, 16,
                "batch=65536 envs x 31x31 viewport in 32x32 planes (C3), random policy, autoreset"),
+    # C5: per step the fused step plus the PragmaticObsWrapper features (wab_featurize) into a
+    # [T, B, 449] rollout buffer, reward/done straight into [T, B]; every T steps the
+    # discounted-return scan (wab_discounted_returns) over the segment
+    "c5": ({}, 0, 8, "batch=65536 envs x default options, actor-critic rollout (C5): step + "
+                     "PragmaticObsWrapper features + discounted returns every %d steps, random policy"),
 }
+C5_SEGMENT = 32  # rollout segment length T (actor_critic.py collects one episode, <= 80 steps)
 
 
 def committed_traffic(config, batch):
@@ -49,29 +55,47 @@ def alg_bytes_per_env_step(W, H):
     return 3 * W * H + 81
 
 
-def cpu_baseline(opts, stride, seconds, threads):
-    """The C oracle (scalar port of the reference step) timed on this host's cores."""
+def featurize_alg_bytes(W, H, F):
+    """wab_featurize per env: reads the 3*W*H obs bytes and 3 scalar bytes, writes F float32."""
+    return 3 * W * H + 3 + 4 * F
+
+
+# wab_discounted_returns per env-step: reads reward f32 + done u8, writes the f32 return
+RETURNS_ALG_BYTES = 9
+
+
+def cpu_baseline(opts, stride, seconds, threads, with_features=False):
+    """The C oracle (scalar port of the reference step) timed on this host's cores; for C5 each
+    step is followed by the oracle's PragmaticObsWrapper featurizer (one thread)."""
     import numpy as np
 
-    from oracle.oracle import OracleBatch
+    from oracle import oracle as O
 
     Bc = 4096
-    orc = OracleBatch(opts, Bc, 0x5EED, 0, True, stride)
+    orc = O.OracleBatch(opts, Bc, 0x5EED, 0, True, stride)
     orc.reset()
     rng = np.random.RandomState(0)
     acts = [rng.randint(orc.n_actions, size=Bc).astype(np.int8) for _ in range(64)]
-    orc.step(acts[0], nthreads=threads)
+    vm = np.zeros((Bc, 11, 11), np.uint8)
+
+    def one(a):
+        orc.step(a, nthreads=threads)
+        if with_features:
+            O.featurize(orc.planes, orc.food_turns, orc.role, orc.status, vm, orc.W, orc.H)
+
+    one(acts[0])
     n, t0 = 0, time.perf_counter()
     while True:
-        orc.step(acts[n % 64], nthreads=threads)
+        one(acts[n % 64])
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    what = "step + featurize (1 thread)" if with_features else "step"
     return {"value": round(Bc * n / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "oracle/wab_oracle.c, %d envs x %d steps (%.1f s) of the same workload, "
-                      "OpenMP over envs" % (Bc, n, el) if threads > 1 else
-                      "oracle/wab_oracle.c, %d envs x %d steps (%.1f s), 1 thread" % (Bc, n, el)}
+            "sample": "oracle/wab_oracle.c %s, %d envs x %d steps (%.1f s) of the same workload, "
+                      "OpenMP over envs" % (what, Bc, n, el) if threads > 1 else
+                      "oracle/wab_oracle.c %s, %d envs x %d steps (%.1f s), 1 thread" % (what, Bc, n, el)}
 
 
 def main():
@@ -101,7 +125,12 @@ def main():
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
 
     opts, stride, slots, desc = CONFIGS[args.config]
+    c5 = args.config == "c5"
     B, K, W = args.batch, args.steps, args.warmup
+    if c5:
+        desc = desc % C5_SEGMENT
+        K = max(C5_SEGMENT, K // C5_SEGMENT * C5_SEGMENT)  # whole segments
+        W = max(C5_SEGMENT, W // C5_SEGMENT * C5_SEGMENT)
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
                                     env_id_base=env_id_base(rank, B),
                                     autoreset=True, validate_actions=False, plane_stride=stride,
@@ -113,15 +142,34 @@ def main():
     L = _lib.load()
     h = env._h
     obs_addr = ctypes.addressof(env._obs["struct"])
-    rew, done = env.reward.data_ptr(), env.done.data_ptr()
     a0 = actions.data_ptr()
+    rew, done = env.reward.data_ptr(), env.done.data_ptr()
+    if c5:
+        T = C5_SEGMENT
+        F = int(L.wab_feature_dim(h))
+        feats = torch.empty((T, B, F), dtype=torch.float32, device=dev)
+        seg_rew = torch.zeros((T, B), dtype=torch.float32, device=dev)
+        seg_done = torch.zeros((T, B), dtype=torch.uint8, device=dev)
+        seg_ret = torch.empty((T, B), dtype=torch.float32, device=dev)
+        f0, r0, d0, ret0 = feats.data_ptr(), seg_rew.data_ptr(), seg_done.data_ptr(), seg_ret.data_ptr()
 
-    def run(t0, n, stream):
-        s = ctypes.c_void_p(stream.cuda_stream)
-        for t in range(t0, t0 + n):
-            rc = L.wab_step(h, a0 + t * B, obs_addr, rew, done, None, s)
-            if rc:
-                _lib.check(rc, "wab_step")
+        def run(t0, n, stream):
+            s = ctypes.c_void_p(stream.cuda_stream)
+            for t in range(t0, t0 + n):
+                i = t % T
+                _lib.check(L.wab_step(h, a0 + t * B, obs_addr, r0 + 4 * i * B, d0 + i * B, None, s),
+                           "wab_step")
+                _lib.check(L.wab_featurize(h, obs_addr, None, f0 + 4 * i * B * F, s), "wab_featurize")
+                if i == T - 1:
+                    _lib.check(L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s),
+                               "wab_discounted_returns")
+    else:
+        def run(t0, n, stream):
+            s = ctypes.c_void_p(stream.cuda_stream)
+            for t in range(t0, t0 + n):
+                rc = L.wab_step(h, a0 + t * B, obs_addr, rew, done, None, s)
+                if rc:
+                    _lib.check(rc, "wab_step")
 
     stream = torch.cuda.current_stream(dev)
     run(0, W, stream)
@@ -173,11 +221,38 @@ def main():
         evs[i][1].record(stream)
     torch.cuda.synchronize(dev)
     single_ms = sorted(a.elapsed_time(b) for a, b in evs)[n_k // 2]
+    kernel_name = "wab_step_%s (fused step)" % L.wab_step_kernel(h).decode()
+    alg = alg_bytes_per_env_step(env.W, env.H)
+    c5_line = None
+    if c5:
+        # C5 runs three kernels; each one's average launch comes from back-to-back launches of
+        # that kernel alone (HIP events on the launch stream, after the timed region)
+        def per_launch(fn, n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(n):
+                _lib.check(fn(i), "c5 kernel timing")
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            return e0.elapsed_time(e1) / n
+
+        n_k = min(K, 512)
+        step_ms = per_launch(lambda i: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_k)
+        feat_ms = per_launch(lambda i: L.wab_featurize(h, obs_addr, None, f0 + 4 * (i % T) * B * F, s), n_k)
+        ret_ms = per_launch(lambda i: L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s), 64)
+        feat_alg = featurize_alg_bytes(env.W, env.H, F)
+        c5_line = {"segment": T, "feature_dim": F, "step_us": round(step_ms * 1e3, 3),
+                   "featurize_us": round(feat_ms * 1e3, 3), "returns_us_per_segment": round(ret_ms * 1e3, 3),
+                   "alg_bytes_per_env_step": alg + feat_alg + RETURNS_ALG_BYTES,
+                   "achieved_GBs_whole_step": round((alg + feat_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
+        if feat_ms > step_ms:  # the dominant kernel carries the roofline object
+            kernel_name, alg, kern_ms = "wab_featurize_kernel (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
+        else:
+            kern_ms = step_ms
     counters = env.counters()
 
     if rank == 0:
         Wv, Hv = env.W, env.H
-        alg = alg_bytes_per_env_step(Wv, Hv)
         achieved = alg * B / (kern_ms * 1e-3) / 1e9
         value = world * B * K / elapsed
         traffic, traffic_src = committed_traffic(args.config, B)
@@ -203,18 +278,21 @@ def main():
                          "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                          "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg * B,
-                         "kernel": "wab_step_%s (fused step)" % L.wab_step_kernel(h).decode(),
+                         "kernel": kernel_name,
                          "kernel_us": round(kern_ms * 1e3, 3),
-                         "kernel_us_single_launch_median": round(single_ms * 1e3, 3),
                          "alg_bytes_per_env_step": alg},
             "stream_us_per_step": round(stream_ms * 1e3 / K, 3),
             "episodes_finished": counters["resets"],
             "overflow": {"wolf": counters["wolf_overflow"], "eaten": counters["eaten_overflow"]},
         }
+        if c5:
+            line["c5"] = c5_line
+        else:
+            line["roofline"]["kernel_us_single_launch_median"] = round(single_ms * 1e3, 3)
         if world == 1 and not args.no_cpu:
             ncpu = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, ncpu)
-            line["cpu_baseline_1t"] = cpu_baseline(opts, stride, args.cpu_seconds / 2, 1)
+            line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, ncpu, c5)
+            line["cpu_baseline_1t"] = cpu_baseline(opts, stride, args.cpu_seconds / 2, 1, c5)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -220,6 +220,11 @@ int wab_egocentric(wab_handle* h, const uint8_t* mask, uint8_t* proximity, void*
 int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, int64_t B,
                            double gamma, const float* bootstrap, float* returns, void* stream);
 
+/* Test hook: the bush value (berries, generate_n_bush_values wab_env.py:631-635) the step
+ * kernels give the 53-bit draws U[n] under h's threshold table, computed by the kernels' own
+ * bracketed search (bush_value_fast).  U, out device pointers. */
+int wab_debug_bush_values(wab_handle* h, const uint64_t* U, int32_t* out, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

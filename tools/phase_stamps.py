@@ -171,6 +171,11 @@ def small_report(env, st, g, steps):
     acc = {k: [] for k in waves}
     spans, ends = [], []
     by_xcd, slow_w0, fast_w0, start_off = [], [], [], []
+    # extra stamps: W2 28 after B_init, 29 after despawn; W1 30 after B_init, 31 after the key
+    DETAIL = {"W2 start->B_init": (16, 28), "W2 B_init->despawned": (28, 29), "W2 despawned->grid": (29, 17),
+              "W1 start->B_init": (10, 30), "W1 key": (30, 31), "W1 tile value": (31, 11),
+              "W0 start->W2 B_init": (0, 28)}
+    detail = []
     for t in range(steps):
         st.zero_()
         env.step(torch.randint(0, env.n_actions, (B,), device="cuda:0", generator=g))
@@ -192,11 +197,13 @@ def small_report(env, st, g, steps):
         slow_w0.append(d0[order[-len(order) // 20:]].mean(axis=0))
         fast_w0.append(d0[order[: len(order) // 4]].mean(axis=0))
         start_off.append(((s[:, 0] - t0)[order[-len(order) // 20:]].mean(), (s[:, 0] - t0)[order[: len(order) // 4]].mean()))
+        detail.append([(s[:, a1] - s[:, a0]).mean() for a0, a1 in DETAIL.values()])
     for k, (cols, names) in waves.items():
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s:" % k)
         for n, v in zip(names, a):
             print("  %-28s %7.2f us" % (n, v))
+    print("detail (us):", ", ".join("%s %.2f" % (n, v * 10 / 1000) for n, v in zip(DETAIL, np.mean(detail, axis=0))))
     print("%-24s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
     print("workgroup end times p0/p50/max (us):", np.round(np.mean(ends, axis=0) * 10 / 1000, 2))
     print("mean end time by blockIdx %% 8 (us):", np.round(np.mean(by_xcd, axis=0) * 10 / 1000, 2))

@@ -15,6 +15,7 @@
 
 #include "../../include/wab.h"
 #include "wab_params.h"
+#include "wab_device.h"
 
 namespace wab {
 template <int MODE, int SLOTS, bool SMALL>
@@ -208,6 +209,19 @@ int launch(wab_handle* h, const Params& p, hipStream_t stream) {
   return WAB_OK;
 }
 
+// wab_debug_bush_values: the step kernels' bush value (bush_value_fast over the padded LDS
+// table) of arbitrary draws
+__global__ __launch_bounds__(256) void bush_values_kernel(const uint64_t* thresholds, int n_thr, float power,
+                                                          const uint64_t* U, int32_t* out, int64_t n) {
+  __shared__ uint64_t tab[256 + 4];
+  uint64_t* thr = tab + 1;
+  for (int k = threadIdx.x; k < n_thr; k += 256) thr[k] = thresholds[k];
+  if (threadIdx.x == 0) wab::bush_thr_pads(thr, n_thr);
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = wab::bush_value_fast(thr, n_thr, U[i], power);
+}
+
 // "U >= T" with U = hi << 21 | lo21 becomes (hi, lo21) >= (th, tl); T >= 2^53 never holds
 void split_threshold(uint64_t T, uint32_t* th, uint32_t* tl) {
   if (T >= (1ull << 53)) {
@@ -303,6 +317,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   const uint64_t keep_ge = (uint64_t)std::floor(std::ldexp(c->wolf_chance_to_despawn, 53)) + 1;  // u > p (:263)
   const uint64_t spawn_ge = (uint64_t)std::ceil(std::ldexp(c->chance_wolf_on_square / 2.0, 53));  // u < p/2 (:573)
   p.max_berries = c->max_berries_per_bush;
+  p.bush_power = (float)c->bush_power;
   const uint64_t bush_ge = p.max_berries > 0 ? c->bush_thresholds[0] : (1ull << 53);          // food > 0
   split_threshold(keep_ge, &p.keep_th, &p.keep_tl);
   split_threshold(spawn_ge, &p.spawn_th, &p.spawn_tl);
@@ -723,6 +738,17 @@ int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, 
   if (T == 0 || B == 0) return WAB_OK;
   hipLaunchKernelGGL(wab::wab_returns_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns);
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+
+int wab_debug_bush_values(wab_handle* h, const uint64_t* U, int32_t* out, int64_t n, void* stream) {
+  g_err.clear();
+  if (!h || !U || !out || n < 0) return fail(WAB_E_INVALID, "wab_debug_bush_values: bad argument");
+  if (n == 0) return WAB_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(bush_values_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, h->p.thresholds,
+                     h->p.max_berries, h->p.bush_power, U, out, n);
   HIP_TRY(hipGetLastError());
   return WAB_OK;
 }

@@ -81,6 +81,31 @@ __device__ __forceinline__ int bush_value(const uint64_t* thr, int n, uint64_t U
   return base + c2;
 }
 
+// The same count from a float guess: c = round(n * u^power) is within 1 of the count for any
+// draw (the guess is off by ~1e-4 at power 100), so four thresholds pin it.  With T_0 = 0 and
+// T_k = +inf for k > n, "T_k <= U" holds exactly for k <= count, so T_{c-1} <= U < T_{c+2}
+// proves count in [c-1, c+1], and then count = c - 2 + #{k in c-1..c+1 : T_k <= U}.  A lane
+// whose guess misses that bracket falls back to the search above: the result is exact
+// whatever the guess.  Layout (bush_thr_pads): thr[k - 1] = T_k, thr[-1] = 0, thr[n] =
+// thr[n + 1] = ~0.
+__device__ __forceinline__ int bush_value_fast(const uint64_t* thr, int n, uint64_t U, float power) {
+  if (n <= 0) return 0;
+  const float u = (float)(uint32_t)(U >> 21) * 0x1p-32f;
+  const float guess = (float)n * __builtin_amdgcn_exp2f(power * __builtin_amdgcn_logf(u));
+  const int c = min(max((int)__builtin_rintf(guess), 1), n);  // (log2(0) = -inf: guess 0)
+  const uint64_t t0 = thr[c - 2], t1 = thr[c - 1], t2 = thr[c], t3 = thr[c + 1];
+  int v = c - 2 + (t0 <= U ? 1 : 0) + (t1 <= U ? 1 : 0) + (t2 <= U ? 1 : 0);
+  if (!(t0 <= U && t3 > U)) v = bush_value(thr, n, U);
+  return v;
+}
+
+// the pads of bush_value_fast's table around thr[0 .. n) (one lane)
+__device__ __forceinline__ void bush_thr_pads(uint64_t* thr, int n) {
+  thr[-1] = 0ull;
+  thr[n] = ~0ull;
+  thr[n + 1] = ~0ull;
+}
+
 // packed-tile add: both int16 halves wrap independently (v_pk_add_u16)
 typedef unsigned short wab_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t xy_add(uint32_t a, uint32_t b) {

@@ -54,6 +54,7 @@ struct Params {
   const uint32_t* tables;      // device: [WH] view-cell world offsets (cw - i, ch - j), then from
   int32_t ring_at;             //   ring_at (16-B aligned) the R ring offsets, padded to a multiple of 4
   int32_t max_berries;
+  float bush_power;            // the guess of bush_value_fast (the thresholds decide)
   double fill, hunger;
   double r_turn, r_killed, r_starve, r_finish, r_eat;
   double start_food;
@@ -132,7 +133,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   SmallLayout L;
   uint32_t o = 0;
   L.tiles = o; o += lds_align4((uint32_t)p.WH);
-  L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
+  L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.stream_words = lds_align4((64u * (uint32_t)p.OB + 31u) >> 5);
   L.stream = o; o += L.stream_words + 4u;  // + slack for stream_or128's fifth dword
   L.cval = o; o += 64u;
@@ -168,7 +169,7 @@ __host__ __device__ inline WideLayout wide_layout(const Params& p) {
   L.spw = (((uint32_t)p.R + 31u) >> 5) | 1u;  // spawn-mask dwords per env (odd pitch)
   L.spawn = o; o += lds_align4(64u * L.spw);
   L.ring = o; o += lds_align4((uint32_t)p.R);  // spawn-ring offsets
-  L.thr = o; o += lds_align4(2u * (uint32_t)p.max_berries);
+  L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.cval = o; o += 64u;                       // generated berries of the ostrich's tile
   L.info = o; o += 64u;                       // W0 -> all: job | emptied << 1
   L.blk = o; o += 4u;                         // n_jobs, job mask lo, hi

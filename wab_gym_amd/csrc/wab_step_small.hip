@@ -164,7 +164,7 @@ __device__ __forceinline__ void ring_part(const Params& p, const Head& h, uint32
 }
 
 // the spawn ring split in twelfths (multiples of 4), balanced against each wave's other work
-// before B1: W0 [0, 2/12), W1 [2/12, 4/12), W2 [4/12, 7/12), W3 [7/12, 1)
+// before B1: W0 [0, 2/12), W1 [2/12, 4/12), W2 [4/12, 6/12), W3 [6/12, 1)
 __device__ __forceinline__ int ring_cut(const Params& p, int k) { return min(p.R, ((p.R * k / 12) + 3) & ~3); }
 
 // reset draws (generate_bushes, initialize_wolves) of every job for view cells
@@ -247,7 +247,7 @@ __device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint
 
 struct Lds {
   uint32_t* tiles;  // [WH] view-cell world offsets (reset draws, initial wolves)
-  uint64_t* thr;    // [max_berries] bush thresholds (W1)
+  uint64_t* thr;    // [max_berries] bush thresholds (W1), padded (bush_thr_pads)
   uint32_t* stream; // 64 envs x OB bits: bit k = byte k of the group's obs chunk
   uint32_t* cval;   // [64] generated berries of the ostrich's tile (W1), then flag[0] = 1
   uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done; zeroed by W0 before B_init
@@ -264,7 +264,7 @@ struct Lds {
 __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   Lds s;
   s.tiles = lds + L.tiles;
-  s.thr = reinterpret_cast<uint64_t*>(lds + L.thr);
+  s.thr = reinterpret_cast<uint64_t*>(lds + L.thr) + 1;
   s.stream = lds + L.stream;
   s.cval = lds + L.cval;
   s.flag = lds + L.flag;
@@ -554,12 +554,24 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   SMALL_STAMP(10);
   __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
   const Head h = head_load(p, g, g < p.B);
-  for (int k = lane; k < p.max_berries; k += 64) s.thr[k] = p.thresholds[k];
+  {  // every threshold load in flight at once (a copy loop waits for each before the next)
+    const int nthr = p.max_berries;  // <= 255
+    uint64_t tv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (64 * k + lane < nthr) s.thr[64 * k + lane] = tv[k];
+    if (lane == 0) bush_thr_pads(s.thr, nthr);
+  }
   lds_barrier();  // B_init
+  SMALL_STAMP(30);
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
+  SMALL_STAMP(31);
   // the generated berries of the ostrich's tile (:631-635), for W0
-  s.cval[lane] = (uint32_t)bush_value(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1));
+  s.cval[lane] =
+      (uint32_t)bush_value_fast(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1), p.bush_power);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_store(s.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __builtin_amdgcn_s_setprio(0);
@@ -624,6 +636,7 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   }
   const Head h = head_load(p, g, active);
   lds_barrier();  // B_init
+  SMALL_STAMP(28);
   const int nw = (int)misc_nw(h.hdr.z);
 #pragma unroll
   for (int k = 4; k < SLOTS; ++k)
@@ -669,6 +682,7 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
     }
     live = keep;
   }
+  SMALL_STAMP(29);
   // pursuit (:267-286): one axis step toward the ostrich, ties along x; grid of S; kill
   M128 wolfp = {0ull, 0ull};
   bool kill = false;
@@ -698,7 +712,7 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   SMALL_STAMP(17);
   // ring part B
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 4), ring_cut(p, 7), spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 4), ring_cut(p, 6), spawn);
   s.spawn[64 + lane] = m_pack(spawn);
   SMALL_STAMP(18);
   lds_barrier();  // B1: every ring part, the starve flags and the bushes' counts are in
@@ -753,7 +767,16 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
   const Head h = head_load(p, g, g < p.B);
-  for (int c = lane; c < p.WH; c += 64) s.tiles[c] = p.tables[c];
+  if constexpr (G == 11) {  // view-cell offsets (cw - i, ch - j) of cell c = 11 i + j, computed
+    for (int c = lane; c < 121; c += 64) s.tiles[c] = xy_pack(5 - c / 11, 5 - c % 11);
+  } else {
+    uint32_t tv[2];  // WH <= 128: both loads in flight at once
+#pragma unroll
+    for (int k = 0; k < 2; ++k) tv[k] = p.tables[min(64 * k + lane, p.WH - 1)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (64 * k + lane < p.WH) s.tiles[64 * k + lane] = tv[k];
+  }
   {  // zero the reset tables (jbm, jwm: [64][4] each, contiguous)
     uint4* z = reinterpret_cast<uint4*>(s.jbm);
     for (int i = lane; i < 2 * 64; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -763,7 +786,7 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
   // ring part C
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 7), p.R, spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 6), p.R, spawn);
   s.spawn[128 + lane] = m_pack(spawn);
   SMALL_STAMP(23);
   lds_barrier();  // B1

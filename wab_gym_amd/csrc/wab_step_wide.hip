@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   uint32_t* wp = lds + L.wp;
   uint32_t* spawn = lds + L.spawn;
   uint32_t* ring = lds + L.ring;
-  uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr);
+  uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr) + 1;  // padded (bush_thr_pads)
   uint32_t* cval = lds + L.cval;
   uint32_t* info = lds + L.info;
   uint32_t* blk = lds + L.blk;
@@ -522,6 +522,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
+        if (lane == 0) bush_thr_pads(thr, nthr);
         WIDE_STAMP(15);
         const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
         const uint32_t top = 1u << (p.H - 1);
@@ -563,7 +564,8 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         __builtin_amdgcn_wave_barrier();
         uint32_t cv = 0;
         if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
-          cv = (uint32_t)bush_value(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1));
+          cv = (uint32_t)bush_value_fast(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1),
+                                         p.bush_power);
         cval[lane] = cv;
         __builtin_amdgcn_s_setprio(0);
       } else {
