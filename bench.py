@@ -246,7 +246,9 @@ def main():
                    "alg_bytes_per_env_step": alg + feat_alg + RETURNS_ALG_BYTES,
                    "achieved_GBs_whole_step": round((alg + feat_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
         if feat_ms > step_ms:  # the dominant kernel carries the roofline object
-            kernel_name, alg, kern_ms = "wab_featurize_kernel (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
+            fk = ("wab_featurize_small_kernel" if env.W * env.H <= 128 and env.S == env.H
+                  else "wab_featurize_kernel")
+            kernel_name, alg, kern_ms = fk + " (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
         else:
             kern_ms = step_ms
     counters = env.counters()

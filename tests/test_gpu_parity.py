@@ -254,6 +254,55 @@ def test_featurizer_matches_reference_golden():
     assert np.array_equal(f.cpu().numpy(), z["features"])
 
 
+def test_featurizer_small_kernel_golden_subsets():
+    """Views of <= 128 cells without a caller-given mask use wab_featurize_small_kernel: the
+    golden grids whose mask is all zero (no restrict_view) or the role's restrict_view mask."""
+    import torch
+
+    from wab_gym_amd.options import view_masks
+    from wab_gym_amd.wrappers import PragmaticObsWrapper
+
+    z = np.load(gr.GOLDEN_DIR + "/pragmatic.npz")
+    vm, sc = z["view_mask"], z["scalars"]
+    for opts in (None, {"restrict_view": True, "lookout_only": False}):
+        if opts is None:
+            sel = np.nonzero(vm.reshape(len(vm), -1).sum(1) == 0)[0]
+        else:
+            table = view_masks(dict(opts))
+            sel = np.nonzero([np.array_equal(vm[i], table[sc[i, 1]]) for i in range(len(vm))])[0]
+        assert len(sel) > 400
+        env = _env(opts, len(sel))
+        wrap = PragmaticObsWrapper(env)
+        planes = torch.as_tensor(z["planes"][sel]).cuda()
+        scal = torch.as_tensor(np.ascontiguousarray(sc[sel].T)).cuda()
+        f = wrap.observation({"planes": planes, "scalars": scal})
+        assert np.array_equal(f.cpu().numpy(), z["features"][sel])
+
+
+@pytest.mark.parametrize("wh", [(11, 11), (9, 9), (7, 13), (13, 9), (5, 5)])
+def test_featurizer_small_kernel_random_planes(wh):
+    """Random planes at densities from sparse to full (ties at every distance) against the
+    oracle, for both wrappers, including a partial last block."""
+    import torch
+
+    from oracle import oracle as orc
+    from wab_gym_amd.wrappers import PragmaticObsWrapper, SuperBasicObservationWrapper
+
+    W, H = wh
+    n = 64 * 37 + 23
+    rng = np.random.default_rng(W * 100 + H)
+    dens = rng.choice([0.0, 0.01, 0.05, 0.2, 0.5, 0.9, 1.0], size=(n, 1, 1, 1))
+    planes = (rng.random((n, 3, W, H)) < dens).astype(np.uint8)
+    sc = np.stack([rng.integers(0, 41, n), rng.integers(0, 2, n), rng.integers(0, 3, n)]).astype(np.uint8)
+    env = _env({"width": W, "height": H}, n)
+    obs = {"planes": torch.as_tensor(planes).cuda(), "scalars": torch.as_tensor(sc).cuda()}
+    f = PragmaticObsWrapper(env).observation(obs)
+    want = orc.featurize(planes, sc[0], sc[1], sc[2], np.zeros((n, 11, 11), np.uint8), W, H)
+    assert np.array_equal(f.cpu().numpy(), want)
+    f = SuperBasicObservationWrapper(env).observation(obs)
+    assert np.array_equal(f.cpu().numpy(), orc.featurize_superbasic(planes, sc[0], sc[1], sc[2], W, H))
+
+
 def test_featurizer_on_env_obs_matches_oracle():
     import torch
 

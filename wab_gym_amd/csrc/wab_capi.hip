@@ -25,28 +25,8 @@ __global__ void wab_step_small(Params p);
 template <int MODE, int SLOTS>
 __global__ void wab_step_wide(Params p);
 
-struct FeatParams {
-  int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
-  int32_t kind;
-  int64_t B;
-  uint32_t mask_rows[2][11];
-  const uint8_t* planes;
-  const uint8_t* food_turns;
-  const uint8_t* role;
-  const uint8_t* status;
-  const uint8_t* view_mask;
-  float* out;
-};
 __global__ void wab_featurize_kernel(FeatParams p);
-struct RenderParams {
-  int32_t W, H, S, OB, scale, restrict_view;
-  int64_t B;
-  uint32_t mask_rows[2][11];
-  const uint8_t* planes;
-  const uint8_t* role;
-  const uint8_t* status;
-  uint8_t* rgb;
-};
+__global__ void wab_featurize_small_kernel(FeatParams p);
 __global__ void wab_render_kernel(RenderParams p);
 __global__ void wab_egocentric_kernel(EgoParams p);
 __global__ void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T, int64_t B,
@@ -617,10 +597,29 @@ int featurize(wab_handle* h, int kind, const wab_obs* obs, const uint8_t* view_m
   fp.status = obs->status;
   fp.view_mask = view_mask;
   fp.out = features;
+  for (int r = 0; r < 2; ++r)  // the view mask as 121 cell bits, bit i*11 + j
+    for (int i = 0; i < 11; ++i)
+      for (int j = 0; j < 11; ++j)
+        if ((p.mask_rows[r][i] >> j) & 1u) fp.view121[r][(i * 11 + j) >> 5] |= 1u << ((i * 11 + j) & 31);
   if (h->n_blocks == 0) return WAB_OK;
-  const uint32_t inW = (uint32_t)(64 * p.OB + 31) / 32, outW = (uint32_t)(64 * F + 31) / 32;
-  const size_t lds = (size_t)(((inW + 3) & ~3u) + outW) * 4;
   DeviceGuard guard(h->device);
+  // views whose planes fit 128 bits in unpadded rows: the table-driven kernel
+  // (wab_featurize_small_kernel); a caller-given view mask or larger views: the general one.
+  // The wrapper measures rows from H//2 and columns from W//2 (:779-780); on non-square views
+  // that distance can reach md, beyond the small kernel's rings: those take the general one too.
+  int max_dist = 0;
+  for (int r = 0; r < p.W; ++r)
+    for (int c = 0; c < p.H; ++c) max_dist = std::max(max_dist, std::abs(r - p.H / 2) + std::abs(c - p.W / 2));
+  const bool small = p.W * p.H <= 128 && p.S == p.H && !view_mask && max_dist < fp.md;
+  const uint32_t inW = (uint32_t)(64 * p.OB + 31) / 32, outW = (uint32_t)(64 * F + 31) / 32;
+  if (small) {
+    const uint32_t a = (inW + 4 + 3) & ~3u, b = (outW + 4 + 3) & ~3u;
+    const size_t lds = (size_t)(a + b + 128 + 4 * (fp.md + 4)) * 4;
+    hipLaunchKernelGGL(wab::wab_featurize_small_kernel, dim3(h->n_blocks), dim3(256), lds, (hipStream_t)stream, fp);
+    HIP_TRY(hipGetLastError());
+    return WAB_OK;
+  }
+  const size_t lds = (size_t)(((inW + 3) & ~3u) + outW) * 4;
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<void*>(&wab::wab_featurize_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -199,4 +199,30 @@ struct EgoParams {
   unsigned long long* counters;  // [3]: path entries missing (stale or beyond cap)
 };
 
+// wab_featurize / wab_featurize_superbasic (wab_features.hip)
+struct FeatParams {
+  int32_t W, H, S, OB, md, F, turns_empty, restrict_view;
+  int32_t kind;  // 0 PragmaticObsWrapper (:726-824), 1 SuperBasicObservationWrapper (:900-927)
+  int64_t B;
+  uint32_t mask_rows[2][11];
+  uint32_t view121[2][4];    // the same masks as 121-bit cell masks (bit i*11 + j)
+  const uint8_t* planes;
+  const uint8_t* food_turns;
+  const uint8_t* role;
+  const uint8_t* status;
+  const uint8_t* view_mask;  // [B][11][11] or null (derive from role)
+  float* out;                // [B][F]
+};
+
+// wab_render (wab_render.hip)
+struct RenderParams {
+  int32_t W, H, S, OB, scale, restrict_view;
+  int64_t B;
+  uint32_t mask_rows[2][11];
+  const uint8_t* planes;
+  const uint8_t* role;
+  const uint8_t* status;
+  uint8_t* rgb;
+};
+
 }  // namespace wab

@@ -12,16 +12,6 @@
 
 namespace wab {
 
-struct RenderParams {
-  int32_t W, H, S, OB, scale, restrict_view;
-  int64_t B;
-  uint32_t mask_rows[2][11];
-  const uint8_t* planes;
-  const uint8_t* role;
-  const uint8_t* status;
-  uint8_t* rgb;
-};
-
 __device__ __forceinline__ uint8_t render_byte(const RenderParams& p, int64_t e, uint32_t o) {
   const uint32_t RH = (uint32_t)(p.H * p.scale);
   const uint32_t px = o / 3u, c = o - px * 3u;
