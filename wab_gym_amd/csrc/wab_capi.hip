@@ -426,6 +426,19 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     h->wide_lds_bytes = (size_t)wab::wide_layout(p).total * 4u;
     h->p.obs_nt = 0;  // plain stores measured faster than non-temporal for this pattern
     if (const char* nt = std::getenv("WAB_OBS_NT")) h->p.obs_nt = std::atoi(nt);
+    {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
+      // off by default: measured neutral once W0 writes the wolf planes early (46.9 vs 47.3 us)
+      h->p.age_cus = 0;
+      h->p.age_shift = 0;
+      if (const char* a = std::getenv("WAB_AGE_PRIO")) {  // experiments: k > 0: priority = age >> (k - 1)
+        if (std::atoi(a) > 0) {
+          h->p.age_cus = cus;
+          h->p.age_shift = std::atoi(a) - 1;
+        }
+      }
+    }
     if (const char* kb = std::getenv("WAB_WIDE_LDS_KB"))
       h->wide_lds_bytes = std::max(h->wide_lds_bytes, (size_t)std::atoi(kb) * 1024u);
     for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots)})

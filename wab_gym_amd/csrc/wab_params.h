@@ -62,6 +62,8 @@ struct Params {
   int32_t max_turns, turns_empty;
   int32_t lookout_only, restrict_view, wolves_on, wolves_can_move, god_mode, autoreset;
   int32_t obs_nt;           // wide kernel: obs stores non-temporal (1) or plain (0)
+  int32_t age_shift;        // priority = age >> age_shift
+  int32_t age_cus;          // > 0: issue priority by workgroup age on its CU (blockIdx / age_cus), 0: off
   uint32_t mask_rows[2][11];  // restrict_view: 11-bit row masks per role (bit j <=> mask[i][j])
   uint32_t small_masks[3][4]; // W*H <= 128: column 0, column H-1, valid-bit masks of the bitmap
   uint32_t view121[2][4];     // restrict_view at 11x11: the row masks as one 121-bit plane mask

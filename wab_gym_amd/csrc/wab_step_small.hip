@@ -627,19 +627,23 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   const bool active = g < p.B;
   SMALL_STAMP(16);
+  // the first 8 slots load with the header, whatever the wolf count: a group of 64 envs
+  // nearly always has a lane with more than 4 wolves, and loading the rest after the count
+  // arrives costs a second memory round trip on the path to B1
+  constexpr int kSpecSlots = SLOTS < 8 ? SLOTS : 8;
   uint32_t wr[SLOTS];
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
   if (active) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // slots 0..3 speculatively
+    for (int k = 0; k < kSpecSlots; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
   }
   const Head h = head_load(p, g, active);
   lds_barrier();  // B_init
   SMALL_STAMP(28);
   const int nw = (int)misc_nw(h.hdr.z);
 #pragma unroll
-  for (int k = 4; k < SLOTS; ++k)
+  for (int k = kSpecSlots; k < SLOTS; ++k)
     if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);

@@ -6,16 +6,16 @@
 // four SIMDs, with the remaining hash work overlapping their drain.  One 256-thread
 // workgroup serves 64 envs; each wave runs one lane per env:
 //
-//          W0 dynamics            W1 bushes               W2             W3 ring
-//   P0     state + log loads,     bitmap rows (one dword  first spawn-   ring offsets
-//          despawn, pursuit,      per row), scroll,       ring word      -> LDS
-//          kill, wolf grid of S   entering row/column
-//                                 draws, emptied tiles,
+//          W0 dynamics            W1 bushes               W2 ring         W3
+//   P0     state + log loads,     bitmap rows (one dword  ring offsets    ostrich grids
+//          despawn, pursuit,      per row), scroll,       -> LDS, first   -> obs plane 2
+//          kill, wolf grids of S  entering row/column     spawn-ring
+//          -> obs plane 0         draws, emptied tiles,   word
 //                                 ostrich-tile value
 //   -- B1 --  S (the obs snapshot) is complete
-//   P1     eat, hunger, starve,   obs chunks of S         obs chunks     the rest of
-//          reward/done, scalars,                          of S           the ring
-//          job list; obs chunks
+//   P1     eat, hunger, starve,   obs plane 1 (bushes)    obs plane 1     the rest of
+//          reward/done, scalars,                                          the ring
+//          job list; obs plane 1
 //   -- B2 --
 //   P2     W0: spawns, state stores; all: post-eat bitmaps, terminal obs of done envs
 //   (done envs: B3, reset draws by ballot, B4, new episodes, their obs and bitmaps)
@@ -201,10 +201,13 @@ __device__ __forceinline__ uint32_t chunk_bits(const Params& p, const uint32_t* 
   return (row >> (16u * half)) & 0xFFFFu;
 }
 
-// Obs chunks (16 bytes).  The ostrich grid (plane 2) is the same in every observation (the
-// centre cell), so W3 writes it while the snapshot S is still being built (obs_plane2); the
-// wolf and bush grids (planes 0, 1) of S follow from the threads of waves 0-2 (obs_main).
-// Chunk r < 2*W*S/16 of env e is always written by thread (e * 2WC + r) % kObsThreads, also
+// Obs chunks (16 bytes), one plane at a time, each from the wave(s) that can write it first.
+// The ostrich grid (plane 2) is the same in every observation (the centre cell): W3 writes it
+// from the start (obs_plane2).  The wolf grid of S (plane 0) is complete once W0 has moved
+// the wolves, long before the bush bitmap: W0 writes it then, while W1 still builds S
+// (obs_plane0).  The bush grid (plane 1) follows from the threads of waves 0-2 after B1
+// (obs_plane1).  Plane-k chunk r < W*S/16 of env e is always written by the same thread —
+// W0 lane (e*WC + r) % 64 for plane 0, thread (e*WC + r) % kObsThreads for plane 1 — also
 // when a done env's new-episode obs later overwrites it (obs_env), so both stores come from
 // one thread in program order.
 constexpr uint32_t kObsThreads = 192;
@@ -212,6 +215,12 @@ constexpr uint32_t kObsThreads = 192;
 __device__ __forceinline__ void store16(const Params& p, uint8_t* out, uint32_t q, const u32x4& v) {
   if (p.obs_nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out) + q);
   else reinterpret_cast<u32x4*>(out)[q] = v;
+}
+
+// 16 bits of row chunk r (< WC) of one plane's rows
+__device__ __forceinline__ uint32_t row_chunk(const uint32_t* rows, uint32_t CPR, uint32_t r) {
+  const uint32_t i = CPR == 2u ? r >> 1 : r, half = CPR == 2u ? r & 1u : 0u;
+  return (rows[i] >> (16u * half)) & 0xFFFFu;
 }
 
 __device__ __forceinline__ void obs_plane2(const Params& p, uint8_t* out, uint32_t n_active, int lane) {
@@ -228,27 +237,34 @@ __device__ __forceinline__ void obs_plane2(const Params& p, uint8_t* out, uint32
   }
 }
 
-__device__ __forceinline__ void obs_main(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
-                                         uint32_t n_active, int tid) {
-  const uint32_t CPE = (uint32_t)p.OB >> 4, C2 = 2u * (((uint32_t)p.S >> 4) * (uint32_t)p.W);
-  const uint32_t n = n_active * C2;
+// plane k (0: wolf rows `rows` = wp, by the 64 lanes of W0; 1: bush rows = bm, by threads
+// [0, kObsThreads)) of every env of the group
+template <int K>
+__device__ __forceinline__ void obs_plane(const Params& p, const uint32_t* rows, uint8_t* out, uint32_t n_active,
+                                          int tid) {
+  constexpr uint32_t NT = K == 0 ? 64u : kObsThreads;
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, WC = (uint32_t)p.W * CPR;
+  const uint32_t n = n_active * WC;
   uint32_t e = 0, r = (uint32_t)tid;
-  while (r >= C2) { r -= C2; ++e; }
-  for (uint32_t c = (uint32_t)tid; c < n; c += kObsThreads) {
-    store16(p, out, e * CPE + r, expand16(chunk_bits(p, bm, wp, e, r)));
-    r += kObsThreads;
-    while (r >= C2) { r -= C2; ++e; }
+  while (r >= WC) { r -= WC; ++e; }
+  for (uint32_t c = (uint32_t)tid; c < n; c += NT) {
+    store16(p, out, e * CPE + (uint32_t)K * WC + r, expand16(row_chunk(rows + e * kWidePitch, CPR, r)));
+    r += NT;
+    while (r >= WC) { r -= WC; ++e; }
   }
 }
 
-// planes 0, 1 of one env, same thread mapping as obs_main (threads >= kObsThreads idle)
+// planes 0, 1 of one env, same thread mapping as obs_plane<0> and obs_plane<1>
 __device__ __forceinline__ void obs_env(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
                                         uint32_t e, int tid) {
-  if ((uint32_t)tid >= kObsThreads) return;
-  const uint32_t CPE = (uint32_t)p.OB >> 4, C2 = 2u * (((uint32_t)p.S >> 4) * (uint32_t)p.W);
-  const uint32_t base = e * C2;
-  for (uint32_t r = ((uint32_t)tid + kObsThreads - base % kObsThreads) % kObsThreads; r < C2; r += kObsThreads)
-    store16(p, out, e * CPE + r, expand16(chunk_bits(p, bm, wp, e, r)));
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, WC = (uint32_t)p.W * CPR;
+  const uint32_t base = e * WC;
+  if (tid < 64)
+    for (uint32_t r = ((uint32_t)tid + 64u - base % 64u) % 64u; r < WC; r += 64u)
+      store16(p, out, e * CPE + r, expand16(row_chunk(wp + e * kWidePitch, CPR, r)));
+  if ((uint32_t)tid < kObsThreads)
+    for (uint32_t r = ((uint32_t)tid + kObsThreads - base % kObsThreads) % kObsThreads; r < WC; r += kObsThreads)
+      store16(p, out, e * CPE + WC + r, expand16(row_chunk(bm + e * kWidePitch, CPR, r)));
 }
 
 // all three planes of one env (terminal observations)
@@ -382,6 +398,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         kill |= ddx == 0 && ddy == 0;
       }
       kill = kill && !p.god_mode;
+      // the wolf grids of S are complete (this wave wrote every env's rows): plane 0 now,
+      // while W1 still builds the bush bitmap
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      obs_plane<0>(p, wp, out, (uint32_t)n_active, lane);
       // eaten log, first entries: the ostrich's tile
       int found = -1, found_rem = 0;
 #pragma unroll
@@ -455,9 +476,9 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         blk[1] = (uint32_t)jm;
         blk[2] = (uint32_t)(jm >> 32);
       }
-      __builtin_amdgcn_s_setprio(0);
+      setprio_age(p);
       WIDE_STAMP(3);
-      obs_main(p, bm, wp, out, (uint32_t)n_active, tid);
+      obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       WIDE_STAMP(4);
       lds_barrier();  // B2: job list, spawn masks
       WIDE_STAMP(5);
@@ -567,10 +588,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
           cv = (uint32_t)bush_value_fast(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1),
                                          p.bush_power);
         cval[lane] = cv;
-        __builtin_amdgcn_s_setprio(0);
+        setprio_age(p);
       } else {
         // ---------------------------------------------- W3 P0: the ostrich grids; W2 P0: ring
         // offsets -> LDS, first ring word
+        setprio_age(p);
         if (wave == 3) obs_plane2(p, out, (uint32_t)n_active, lane);
         if (wave == 2) {
           copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
@@ -585,7 +607,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       WIDE_STAMP(8 * wave + 2);
       // ------------------------------------------------ P1: W1, W2 obs of S; W3 the rest of the
       // ring (its VALU work on its own SIMD overlaps the drain of the stores)
-      if (wave < 3) obs_main(p, bm, wp, out, (uint32_t)n_active, tid);
+      if (wave < 3) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       WIDE_STAMP(8 * wave + 3);
       if (wave == 3 && p.wolves_on)
         for (int w = nA; w < RW; ++w)
