@@ -31,9 +31,10 @@ CONFIGS = {
     # 16 wolf slots: with 8, a 961-cell reset view overflows a few times per million resets
     "wide31": ({"width": 31, "height": 31}, 32, 16,
                "batch=65536 envs x 31x31 viewport in 32x32 planes (C3), random policy, autoreset"),
-    # C5: per step the fused step plus the PragmaticObsWrapper features (wab_featurize) into a
-    # [T, B, 449] rollout buffer, reward/done straight into [T, B]; every T steps the
-    # discounted-return scan (wab_discounted_returns) over the segment
+    # C5: per step the step fused with the PragmaticObsWrapper features (wab_step_features) into
+    # a [T, B, 449] rollout buffer, reward/done straight into [T, B]; every T steps the
+    # discounted-return scan (wab_discounted_returns) over the segment (--c5-unfused: wab_step
+    # then wab_featurize)
     "c5": ({}, 0, 8, "batch=65536 envs x default options, actor-critic rollout (C5): step + "
                      "PragmaticObsWrapper features + discounted returns every %d steps, random policy"),
 }
@@ -108,6 +109,8 @@ def main():
     ap.add_argument("--mode", default="graph", choices=["graph", "launch"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c5-unfused", action="store_true",
+                    help="C5 as wab_step + wab_featurize (obs planes stored) instead of wab_step_features")
     args = ap.parse_args()
 
     import torch
@@ -152,14 +155,25 @@ def main():
         seg_done = torch.zeros((T, B), dtype=torch.uint8, device=dev)
         seg_ret = torch.empty((T, B), dtype=torch.float32, device=dev)
         f0, r0, d0, ret0 = feats.data_ptr(), seg_rew.data_ptr(), seg_done.data_ptr(), seg_ret.data_ptr()
+        fused = not args.c5_unfused
+        # the wrapped env of actor_critic.py returns features only: the fused call renders the
+        # obs planes on chip for the featurizer and does not store them
+        o = env._obs["struct"]
+        fobs = _lib.WabObs(None, o.food_turns, o.role, o.status)
+        fobs_addr = ctypes.addressof(fobs)
+
+        def c5_step(t, i, s):
+            if fused:
+                return L.wab_step_features(h, a0 + t * B, fobs_addr, r0 + 4 * i * B, d0 + i * B,
+                                           f0 + 4 * i * B * F, s)
+            rc = L.wab_step(h, a0 + t * B, obs_addr, r0 + 4 * i * B, d0 + i * B, None, s)
+            return rc or L.wab_featurize(h, obs_addr, None, f0 + 4 * i * B * F, s)
 
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
             for t in range(t0, t0 + n):
                 i = t % T
-                _lib.check(L.wab_step(h, a0 + t * B, obs_addr, r0 + 4 * i * B, d0 + i * B, None, s),
-                           "wab_step")
-                _lib.check(L.wab_featurize(h, obs_addr, None, f0 + 4 * i * B * F, s), "wab_featurize")
+                _lib.check(c5_step(t, i, s), "c5 step")
                 if i == T - 1:
                     _lib.check(L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s),
                                "wab_discounted_returns")
@@ -237,15 +251,33 @@ def main():
             return e0.elapsed_time(e1) / n
 
         n_k = min(K, 512)
+        ret_ms = per_launch(lambda i: L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s), 64)
+        if fused:
+            sf_ms = per_launch(lambda i: L.wab_step_features(h, a0 + (W + i) * B, fobs_addr, rew, done,
+                                                             f0 + 4 * (i % T) * B * F, s), n_k)
+            # per env-step: the step's bytes without the planes (never stored), the F floats
+            sf_alg = alg - 3 * env.W * env.H + 4 * F
+            c5_line = {"segment": T, "feature_dim": F, "fused": True,
+                       "step_features_us": round(sf_ms * 1e3, 3),
+                       "returns_us_per_segment": round(ret_ms * 1e3, 3),
+                       "alg_bytes_per_env_step": sf_alg + RETURNS_ALG_BYTES,
+                       "achieved_GBs_whole_step": round((sf_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
+            kernel_name = "wab_step_%s + PragmaticObsWrapper features (wab_step_features)" % L.wab_step_kernel(h).decode()
+            alg, kern_ms = sf_alg, sf_ms
         step_ms = per_launch(lambda i: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_k)
         feat_ms = per_launch(lambda i: L.wab_featurize(h, obs_addr, None, f0 + 4 * (i % T) * B * F, s), n_k)
-        ret_ms = per_launch(lambda i: L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s), 64)
         feat_alg = featurize_alg_bytes(env.W, env.H, F)
-        c5_line = {"segment": T, "feature_dim": F, "step_us": round(step_ms * 1e3, 3),
-                   "featurize_us": round(feat_ms * 1e3, 3), "returns_us_per_segment": round(ret_ms * 1e3, 3),
-                   "alg_bytes_per_env_step": alg + feat_alg + RETURNS_ALG_BYTES,
-                   "achieved_GBs_whole_step": round((alg + feat_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
-        if feat_ms > step_ms:  # the dominant kernel carries the roofline object
+        if fused:
+            c5_line["unfused_step_us"] = round(step_ms * 1e3, 3)
+            c5_line["unfused_featurize_us"] = round(feat_ms * 1e3, 3)
+        else:
+            c5_line = {"segment": T, "feature_dim": F, "fused": False, "step_us": round(step_ms * 1e3, 3),
+                       "featurize_us": round(feat_ms * 1e3, 3), "returns_us_per_segment": round(ret_ms * 1e3, 3),
+                       "alg_bytes_per_env_step": alg + feat_alg + RETURNS_ALG_BYTES,
+                       "achieved_GBs_whole_step": round((alg + feat_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
+        if fused:
+            pass
+        elif feat_ms > step_ms:  # the dominant kernel carries the roofline object
             fk = ("wab_featurize_small_kernel" if env.W * env.H <= 128 and env.S == env.H
                   else "wab_featurize_kernel")
             kernel_name, alg, kern_ms = fk + " (PragmaticObsWrapper + flatten)", feat_alg, feat_ms

@@ -23,6 +23,7 @@
  *   wab_destroy           <- (gym.Env.close; nothing to free in the reference)
  *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
  *   wab_featurize_superbasic <- SuperBasicObservationWrapper.observation wab_env.py:900-927
+ *   wab_step_features        <- PragmaticObsWrapper(env).step, actor_critic.py:180-192
  *   wab_render            <- WolvesAndBushesEnv.render (rgb_array)   wab_env.py:468-502
  *   wab_egocentric        <- WolvesAndBushesEnvEgoCentric._get_obs /  wab_env.py:930-979
  *                            _get_bush_proximities                   wab_env.py:652-667
@@ -190,6 +191,21 @@ int wab_feature_dim(const wab_handle* h);
  * options as _get_obs does (wab_env.py:360-368). */
 int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
                   void* stream);
+
+/* wab_step fused with wab_featurize: PragmaticObsWrapper(WolvesAndBushesEnv).step
+ * (actor_critic.py:180-192 wraps the env, so the policy only ever sees the features;
+ * wab_env.py:670-824 applied to the obs of wab_env.py:250-342).  features [B][F] float32
+ * (F = wab_feature_dim) are those of the obs this step returns (after auto-reset), bit for
+ * bit what wab_step followed by wab_featurize(view_mask = NULL) would produce; reward, done
+ * and the obs scalars are written as by wab_step.  No terminal obs.
+ * obs->planes may be NULL: the planes are then not returned.  When the small-view kernel
+ * steps the handle (wab_step_kernel == "small") and its views fit the table-driven
+ * featurizer, one kernel does both (planes rendered on chip, stored only if asked for);
+ * otherwise the call is wab_step then wab_featurize on `stream` (without caller planes
+ * through a handle-owned buffer the first such call allocates, synchronously).
+ * features (and planes, if set) must be 16-byte aligned. */
+int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward,
+                      uint8_t* done, float* features, void* stream);
 
 /* SuperBasicObservationWrapper.observation (wab_env.py:900-927) + gym flatten: the nearest
  * bush of the bush grid (4 x Discrete(max_distance)), food, role, status -> one-hot float32

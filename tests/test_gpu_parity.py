@@ -326,6 +326,59 @@ def test_featurizer_on_env_obs_matches_oracle():
             assert np.array_equal(f.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("opts,kw", [
+    (None, {}),                                                   # 11x11: G = 11 kernel, 8 slots
+    (None, {"wolf_slots": 32, "autoreset": False}),               # stepping past done
+    ({"restrict_view": True, "lookout_only": False}, {"wolf_slots": 16}),
+    ({"width": 9, "height": 9, "starting_food": None, "starting_role": None}, {}),  # G = 0
+    ({"wolf_spawn_margin": 2}, {}),                               # 104-tile ring, G = 0
+    ({"width": 9, "height": 13}, {}),                             # not fusable: step + featurize
+    ({"width": 31, "height": 31}, {"plane_stride": 32}),          # wide kernel: step + featurize
+])
+def test_step_features_matches_step_then_featurize(opts, kw):
+    """wab_step_features (one kernel where the small kernel steps the handle, obs planes not
+    stored) == wab_step followed by wab_featurize, bit for bit, over 100 steps of a batch with a
+    partial last group; reward, done and the obs scalars too."""
+    import torch
+
+    from wab_gym_amd.wrappers import PragmaticObsWrapper
+
+    n = 1000
+    ea = _env(opts, n, validate_actions=False, **kw)
+    eb = _env(opts, n, validate_actions=False, **kw)
+    wa, wb = PragmaticObsWrapper(ea), PragmaticObsWrapper(eb)
+    fa = torch.full((n, wa.feature_dim), 7.0, device="cuda:0")
+    assert torch.equal(wa.reset(), wb.reset())
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(3)
+    for t in range(100):
+        a = torch.randint(0, ea.n_actions, (n,), device="cuda:0", generator=g)
+        f, ra, da = ea.step_features(a, fa, store_planes=False)
+        _, rb, db, _ = eb.step(a)
+        fb = wb.observation()
+        assert torch.equal(f, fb), t
+        assert torch.equal(ra, rb) and torch.equal(da, db), t
+        assert torch.equal(ea._obs["scalars"], eb._obs["scalars"]), t
+    ca, cb = ea.counters(), eb.counters()
+    assert ca == cb
+
+
+def test_step_features_keeps_planes_when_asked():
+    import torch
+
+    from wab_gym_amd.wrappers import PragmaticObsWrapper
+
+    ea, eb = _env(None, 640), _env(None, 640)
+    wa = PragmaticObsWrapper(ea)
+    wa.reset()
+    eb.reset()
+    for t in range(30):
+        a = torch.full((640,), t % 5, device="cuda:0", dtype=torch.int8)
+        wa.step(a)  # fused, planes stored
+        eb.step(a)
+        assert torch.equal(ea._obs["planes"], eb._obs["planes"]), t
+
+
 def test_superbasic_matches_reference_golden_and_oracle():
     """Device SuperBasicObservationWrapper + flatten == the reference wrapper's golden vectors,
     and == the oracle on live env observations (31x31 included)."""

@@ -17,7 +17,7 @@ EXPORTED = [
     "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
-    "wab_debug_bush_values",
+    "wab_debug_bush_values", "wab_step_features",
 ]
 
 ABI_VERSION = 1
@@ -69,6 +69,7 @@ def load():
     L.wab_featurize.argtypes = [P, P, P, P, P]
     L.wab_superbasic_dim.argtypes = [P]
     L.wab_featurize_superbasic.argtypes = [P, P, P, P]
+    L.wab_step_features.argtypes = [P, P, P, P, P, P, P]
     L.wab_render.argtypes = [P, P, I32, P, P]
     L.wab_egocentric.argtypes = [P, P, P, P]
     L.wab_debug_bush_values.argtypes = [P, P, P, I64, P]

@@ -16,11 +16,12 @@
 #include "../../include/wab.h"
 #include "wab_params.h"
 #include "wab_device.h"
+#include "wab_feat.h"
 
 namespace wab {
 template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
-template <int SLOTS, int G>
+template <int SLOTS, int G, bool FEAT>
 __global__ void wab_step_small(Params p);
 template <int MODE, int SLOTS>
 __global__ void wab_step_wide(Params p);
@@ -43,8 +44,10 @@ struct wab_handle {
   size_t lds_bytes = 0;
   int step_kernel = 0;         // KERNEL_BLOCK / KERNEL_SMALL
   size_t small_lds_bytes = 0;  // LDS of the small-view kernel
+  size_t small_feat_lds_bytes = 0;  // ... with the fused featurizer (wab_step_features), 0: not fusable
   bool reset_done = false;
   std::vector<void*> allocs;
+  uint8_t* scratch_planes = nullptr;  // wab_step_features without planes, not fusable (lazy)
   // egocentric observation (allocated by the first wab_egocentric call)
   uint4* ego_path = nullptr;
   uint32_t* ego_diamond = nullptr;
@@ -153,19 +156,20 @@ void* wide_kernel_ptr(int slots) {
 template <int G>
 void* small_kernel_ptr(int slots) {
   switch (slots) {
-    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8, G>);
-    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16, G>);
-    default: return reinterpret_cast<void*>(&wab::wab_step_small<32, G>);
+    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8, G, false>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16, G, false>);
+    default: return reinterpret_cast<void*>(&wab::wab_step_small<32, G, false>);
   }
 }
 
-template <int G>
+template <int G, bool FEAT = false>
 void launch_small(wab_handle* h, const Params& p, hipStream_t stream) {
   const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
+  const size_t lds = FEAT ? h->small_feat_lds_bytes : h->small_lds_bytes;
   switch (h->slots) {
-    case 8: hipLaunchKernelGGL((wab::wab_step_small<8, G>), grid, block, h->small_lds_bytes, stream, p); break;
-    case 16: hipLaunchKernelGGL((wab::wab_step_small<16, G>), grid, block, h->small_lds_bytes, stream, p); break;
-    default: hipLaunchKernelGGL((wab::wab_step_small<32, G>), grid, block, h->small_lds_bytes, stream, p); break;
+    case 8: hipLaunchKernelGGL((wab::wab_step_small<8, G, FEAT>), grid, block, lds, stream, p); break;
+    case 16: hipLaunchKernelGGL((wab::wab_step_small<16, G, FEAT>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((wab::wab_step_small<32, G, FEAT>), grid, block, lds, stream, p); break;
   }
 }
 
@@ -214,6 +218,25 @@ void split_threshold(uint64_t T, uint32_t* th, uint32_t* tl) {
 }
 
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+// flattened PragmaticObsWrapper length, or WAB_E_INVALID when bushes[md//2, md//2] (wab_env.py:742)
+// is outside the grid
+int feature_dim_of(const Params& p) {
+  const int md = p.W / 2 + p.H / 2 + 1;
+  if (md / 2 >= p.W || md / 2 >= p.H) return WAB_E_INVALID;
+  return wab::pragmatic_dim(md, p.turns_empty);
+}
+
+// the table-driven featurizer (wab_feat.h) applies: planes of <= 128 cells in unpadded rows, and
+// every cell's distance from the centre row H//2 / column W//2 (wab_env.py:779-780) below md
+// (always on square views; non-square ones can reach md, beyond the tables' rings)
+bool feat_small_ok(const Params& p) {
+  const int md = p.W / 2 + p.H / 2 + 1;
+  int max_dist = 0;
+  for (int r = 0; r < p.W; ++r)
+    for (int c = 0; c < p.H; ++c) max_dist = std::max(max_dist, std::abs(r - p.H / 2) + std::abs(c - p.W / 2));
+  return p.W * p.H <= 128 && p.S == p.H && max_dist < md;
+}
 
 int check_obs(const wab_obs* o, const char* what) {
   if (!o || !o->planes || !o->food_turns || !o->role || !o->status)
@@ -349,6 +372,13 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     const bool forced_block = k && std::strcmp(k, "block") == 0;
     h->step_kernel = forced_block ? KERNEL_BLOCK : small_view(p) ? KERNEL_SMALL : wide_view(p) ? KERNEL_WIDE : KERNEL_BLOCK;
     h->small_lds_bytes = (size_t)wab::small_layout(p).total * 4u;
+    // wab_step_features fuses the featurizer into the small kernel when the table-driven
+    // featurizer applies (see featurize): every cell within md of the centre row/column
+    if (h->step_kernel == KERNEL_SMALL && feature_dim_of(p) >= 0 && feat_small_ok(p)) {
+      Params q = p;
+      q.features = reinterpret_cast<float*>(16);  // (layout only)
+      h->small_feat_lds_bytes = (size_t)wab::small_layout(q).total * 4u;
+    }
     const char* g = std::getenv("WAB_SMALL_GENERIC");  // A/B: the runtime-geometry build
     h->small_g11 = geometry_11(p) && !(g && std::atoi(g));
   }
@@ -577,10 +607,7 @@ int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* 
 
 int wab_feature_dim(const wab_handle* h) {
   if (!h) return WAB_E_INVALID;
-  const Params& p = h->p;
-  const int md = p.W / 2 + p.H / 2 + 1;
-  if (md / 2 >= p.W || md / 2 >= p.H) return WAB_E_INVALID;  // bushes[md//2, md//2] (wab_env.py:742)
-  return 16 * (md + 1) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121;
+  return feature_dim_of(h->p);
 }
 
 namespace {
@@ -617,17 +644,13 @@ int featurize(wab_handle* h, int kind, const wab_obs* obs, const uint8_t* view_m
   if (h->n_blocks == 0) return WAB_OK;
   DeviceGuard guard(h->device);
   // views whose planes fit 128 bits in unpadded rows: the table-driven kernel
-  // (wab_featurize_small_kernel); a caller-given view mask or larger views: the general one.
-  // The wrapper measures rows from H//2 and columns from W//2 (:779-780); on non-square views
-  // that distance can reach md, beyond the small kernel's rings: those take the general one too.
-  int max_dist = 0;
-  for (int r = 0; r < p.W; ++r)
-    for (int c = 0; c < p.H; ++c) max_dist = std::max(max_dist, std::abs(r - p.H / 2) + std::abs(c - p.W / 2));
-  const bool small = p.W * p.H <= 128 && p.S == p.H && !view_mask && max_dist < fp.md;
+  // (wab_featurize_small_kernel, feat_small_ok); a caller-given view mask or larger views: the
+  // general one
+  const bool small = feat_small_ok(p) && !view_mask;
   const uint32_t inW = (uint32_t)(64 * p.OB + 31) / 32, outW = (uint32_t)(64 * F + 31) / 32;
   if (small) {
     const uint32_t a = (inW + 4 + 3) & ~3u, b = (outW + 4 + 3) & ~3u;
-    const size_t lds = (size_t)(a + b + 128 + 4 * (fp.md + 4)) * 4;
+    const size_t lds = (size_t)(a + b + wab::feat_tables_words(fp.md)) * 4;
     hipLaunchKernelGGL(wab::wab_featurize_small_kernel, dim3(h->n_blocks), dim3(256), lds, (hipStream_t)stream, fp);
     HIP_TRY(hipGetLastError());
     return WAB_OK;
@@ -645,6 +668,52 @@ int featurize(wab_handle* h, int kind, const wab_obs* obs, const uint8_t* view_m
 int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, float* features,
                   void* stream) {
   return featurize(h, 0, obs, view_mask, features, stream, "wab_featurize");
+}
+
+int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward, uint8_t* done,
+                      float* features, void* stream) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_step_features: NULL handle");
+  if (!h->reset_done) return fail(WAB_E_STATE, "wab_step_features: call wab_reset before the first step");
+  if (!actions || !reward || !done || !features || !obs || !obs->food_turns || !obs->role || !obs->status)
+    return fail(WAB_E_INVALID, "wab_step_features: NULL argument");
+  if (!aligned16(features)) return fail(WAB_E_INVALID, "wab_step_features: features must be 16-byte aligned");
+  if (obs->planes && !aligned16(obs->planes))
+    return fail(WAB_E_INVALID, "wab_step_features: planes must be 16-byte aligned");
+  if (wab_feature_dim(h) < 0) return fail(WAB_E_INVALID, "wab_step_features: the wrapper cannot index this viewport");
+  if (!h->small_feat_lds_bytes) {
+    // no fused kernel for these options: the step, then the featurizer, on the same stream
+    // (without caller planes through a handle-owned buffer, allocated by the first such call)
+    wab_obs o = *obs;
+    if (!o.planes) {
+      if (!h->scratch_planes) {
+        DeviceGuard guard(h->device);
+        void* ptr = nullptr;
+        const size_t bytes = std::max<size_t>(16, (size_t)h->p.B * (size_t)h->p.OB);
+        if (hipMalloc(&ptr, bytes) != hipSuccess) return fail(WAB_E_NOMEM, "wab_step_features: hipMalloc");
+        h->allocs.push_back(ptr);
+        h->scratch_planes = static_cast<uint8_t*>(ptr);
+      }
+      o.planes = h->scratch_planes;
+    }
+    if (int rc = wab_step(h, actions, &o, reward, done, nullptr, stream)) return rc;
+    return wab_featurize(h, &o, nullptr, features, stream);
+  }
+  Params p = h->p;
+  p.actions = actions;
+  p.planes = obs->planes;
+  p.food_turns = obs->food_turns;
+  p.role = obs->role;
+  p.status = obs->status;
+  p.reward = reward;
+  p.done = done;
+  p.features = features;
+  if (h->n_blocks == 0) return WAB_OK;
+  DeviceGuard guard(h->device);
+  if (h->small_g11) launch_small<11, true>(h, p, (hipStream_t)stream);
+  else launch_small<0, true>(h, p, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
 }
 
 int wab_superbasic_dim(const wab_handle* h) {

@@ -1,0 +1,156 @@
+// wab_feat.h — the PragmaticObsWrapper features (wab_env.py:726-824, flattened as
+// actor_critic.py:188 does) of views whose planes fit 128 bits, from an LDS obs bit-stream.
+// Shared by the standalone featurizer (wab_featurize_small_kernel, wab_features.hip) and the
+// fused step + features path of the small-view step kernel (wab_step_small.hip).
+//
+// The scan of _get_nearest_things (:763-810) keeps the top two of the set cells under
+// (distance ascending, np.where index descending): a later cell at equal distance replaces
+// the nearest (:782-791).  So the nearest is the highest set bit of the first non-empty ring
+// of cells at one distance, the second the next bit of that ring or the highest of the next
+// non-empty ring; the direction counts (:812-824) are popcounts of four fixed cell masks.
+// Per-cell tables (built once per workgroup in LDS): the packed encodings of every cell, the
+// cells at each distance, the four count masks.
+#pragma once
+
+#include "wab_small.h"
+
+namespace wab {
+
+__device__ __forceinline__ void fset(uint32_t* s, uint32_t bit) { atomicOr(&s[bit >> 5], 1u << (bit & 31)); }
+
+// feature count of PragmaticObsWrapper + flatten (wab_feature_dim): 16 (md+1) + 88 + 2 +
+// (turns_empty + 1) + 2 + 3 + 121
+__host__ __device__ inline int pragmatic_dim(int md, int turns_empty) { return 16 * (md + 1) + 88 + 2 + (turns_empty + 1) + 2 + 3 + 121; }
+
+struct FeatTables {
+  uint32_t* enc;   // [128] per cell: up | right << 8 | down << 16 | left << 24 (encoded values)
+  uint4* ring;     // [md] cells at distance d
+  uint4* cmask;    // [4] cells counted up, right, down, left
+};
+
+// LDS dwords of the tables
+__host__ __device__ inline uint32_t feat_tables_words(int md) { return 128u + 4u * ((uint32_t)md + 4u); }
+
+__device__ __forceinline__ FeatTables feat_tables_at(uint32_t* lds, int md) {
+  FeatTables t;
+  t.enc = lds;
+  t.ring = reinterpret_cast<uint4*>(lds + 128);
+  t.cmask = t.ring + md;
+  return t;
+}
+
+// Build the tables (their LDS must be zero) with threads [0, nthreads); rows of S = H cells.
+// Rows are measured from H//2 and columns from W//2 (:779-780); the host only picks this
+// path when every such distance is below md (always on square views).
+__device__ __forceinline__ void feat_tables_build(const FeatTables& t, int W, int H, int md, int tid, int nthreads) {
+  for (int c = tid; c < W * H; c += nthreads) {
+    const int r = c / H, col = c - (c / H) * H;
+    const int rr = r - H / 2, rc = col - W / 2;
+    const int up = rr < 0 ? -rr : 0, right = rc > 0 ? rc : 0, down = rr > 0 ? rr : 0, left = rc < 0 ? -rc : 0;
+    t.enc[c] = (uint32_t)(up ? md - up : 0) | ((uint32_t)(right ? md - right : 0) << 8) |
+               ((uint32_t)(down ? md - down : 0) << 16) | ((uint32_t)(left ? md - left : 0) << 24);  // :792-808
+    const uint32_t bit = 1u << (c & 31), w = (uint32_t)c >> 5;
+    atomicOr(reinterpret_cast<uint32_t*>(t.ring + (abs(rr) + abs(rc))) + w, bit);
+    uint32_t* cm = reinterpret_cast<uint32_t*>(t.cmask);
+    if (r < H / 2) atomicOr(&cm[0 * 4 + w], bit);
+    if (col > W / 2) atomicOr(&cm[1 * 4 + w], bit);
+    if (r > H / 2) atomicOr(&cm[2 * 4 + w], bit);
+    if (col < W / 2) atomicOr(&cm[3 * 4 + w], bit);
+  }
+}
+
+// bits [at, at + n) of an LDS bit-stream (n <= 128, four dwords of slack after it)
+__device__ __forceinline__ M128 stream_get128(const uint32_t* s, uint32_t at, uint32_t n) {
+  const uint32_t* d = s + (at >> 5);
+  const uint32_t sh = at & 31u;
+  const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4];
+  M128 m = m_make(__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
+                  __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh));
+  if (n < 128u) {
+    if (n >= 64u) m.hi &= (1ull << (n - 64u)) - 1ull;
+    else { m.hi = 0ull; m.lo &= (1ull << n) - 1ull; }
+  }
+  return m;
+}
+
+__device__ __forceinline__ int m_top(const M128& m) {
+  return m.hi ? 127 - (int)__clzll((long long)m.hi) : (m.lo ? 63 - (int)__clzll((long long)m.lo) : -1);
+}
+__device__ __forceinline__ M128 m_of(const uint4& v) { return m_make(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ int m_popc(const M128& m) { return __popcll(m.lo) + __popcll(m.hi); }
+
+// nearest / second nearest (packed encodings, 0 when absent) and the capped direction
+// counts of plane P
+__device__ __forceinline__ void plane_features(const FeatTables& t, int md, M128 P, uint32_t& near, uint32_t& second,
+                                               int counts[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) counts[k] = min(m_popc(m_and(P, m_of(t.cmask[k]))), 10);
+  int n1 = -1, n2 = -1;
+  for (int d = 0; d < md; ++d) {
+    if (__all(n2 >= 0 || (P.lo | P.hi) == 0ull)) break;  // (wave-uniform exit)
+    const M128 r = m_of(t.ring[d]);
+    M128 m = m_and(P, r);
+    P = m_andn(P, r);
+    const int top = m_top(m);
+    if (n1 < 0) {
+      if (top >= 0) {
+        n1 = top;
+        m_clear(m, (uint32_t)top);
+        n2 = m_top(m);
+      }
+    } else if (n2 < 0) {
+      n2 = top;
+    }
+  }
+  near = n1 >= 0 ? t.enc[n1] : 0u;
+  second = n2 >= 0 ? t.enc[n2] : 0u;
+}
+
+// one plane's 12 one-hot features (plane 0 wolves, 1 bushes) of the env whose row starts at
+// feature bit `at`
+__device__ __forceinline__ void emit_plane(uint32_t* ob, uint32_t at, int plane, int md, uint32_t near,
+                                           uint32_t second, const int counts[4]) {
+  const uint32_t M1 = (uint32_t)md + 1u;
+  const uint32_t base = at + (uint32_t)plane * (8u * M1 + 44u);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fset(ob, base + (uint32_t)k * M1 + ((near >> (8 * k)) & 0xFFu));
+    fset(ob, base + (4u + (uint32_t)k) * M1 + ((second >> (8 * k)) & 0xFFu));
+    fset(ob, base + 8u * M1 + 11u * (uint32_t)k + (uint32_t)counts[k]);
+  }
+}
+
+// standing_on_bush (bushes[md//2, md//2], :742), food turns, role, status, view mask
+__device__ __forceinline__ void emit_scalars(uint32_t* ob, uint32_t at, int md, int turns_empty, uint32_t standing,
+                                             uint32_t ft, uint32_t role, uint32_t status, bool restrict_view,
+                                             const M128& vm) {
+  uint32_t o = at + 16u * ((uint32_t)md + 1u) + 88u;
+  fset(ob, o + standing);
+  o += 2u;
+  fset(ob, o + ft);
+  o += (uint32_t)turns_empty + 1u;
+  fset(ob, o + role);
+  o += 2u;
+  fset(ob, o + status);
+  o += 3u;
+  if (restrict_view) stream_or128(ob, o, vm);  // view_mask of _get_obs (:360-368), 121 bits
+}
+
+// feature bits [0, n_active * F) -> float32 at out (16-byte aligned), 16-byte stores
+__device__ __forceinline__ void store_feature_bits(const uint32_t* ob, float* out, uint32_t nf, int tid, int nthreads) {
+  const uint32_t nq = nf >> 2;
+  for (uint32_t u = (uint32_t)tid; u < nq; u += (uint32_t)nthreads) {
+    const uint32_t q = 4u * u;
+    const uint32_t b = (ob[q >> 5] >> (q & 31u)) & 0xFu;
+    float4 f;
+    f.x = (b & 1u) ? 1.0f : 0.0f;
+    f.y = (b & 2u) ? 1.0f : 0.0f;
+    f.z = (b & 4u) ? 1.0f : 0.0f;
+    f.w = (b & 8u) ? 1.0f : 0.0f;
+    reinterpret_cast<float4*>(out)[u] = f;
+  }
+  for (uint32_t q = 4u * nq + (uint32_t)tid; q < nf; q += (uint32_t)nthreads)
+    out[q] = ((ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
+}
+
+}  // namespace wab

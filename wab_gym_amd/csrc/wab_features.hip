@@ -12,11 +12,9 @@
 //   phase 3  all threads   expand feature bits to float32 with 16-byte coalesced stores
 #include <hip/hip_runtime.h>
 
-#include "wab_small.h"
+#include "wab_feat.h"
 
 namespace wab {
-
-__device__ __forceinline__ void fset(uint32_t* s, uint32_t bit) { atomicOr(&s[bit >> 5], 1u << (bit & 31)); }
 
 // nearest / second nearest / direction counts of one plane (_get_nearest_things :763-810,
 // _get_num_things_each_direction :812-824); plane bits [base, base + W*S) of stream s
@@ -177,89 +175,23 @@ __global__ __launch_bounds__(256) void wab_featurize_kernel(FeatParams p) {
 
 // ------------------------------------------------------------------ small views (W*H <= 128)
 // wab_featurize_small_kernel: the same features for views whose planes fit 128 bits in rows
-// of H bytes (S == H; the default 11x11).  The kernel is store-bound (1796 B written per env
-// against 363 read), so what matters is how soon the stores start: no per-bit loops.
-//   prologue  per-cell tables in LDS: the packed encodings (up, right, down, left) of every
-//             cell, the cells at each taxicab distance (ring masks), the direction-count masks
+// of H bytes (S == H; the default 11x11), table-driven (wab_feat.h).  The kernel is
+// store-bound (1796 B written per env against 363 read), so what matters is how soon the
+// stores start: no per-bit loops.
+//   prologue  per-cell tables in LDS (wab_feat.h)
 //   phase 1   16-byte loads, 16 bytes -> one 16-bit LDS store (no zeroing, no atomics)
 //   phase 2   lane = env, one plane per wave: W0 wolves, W1 bushes (+ standing on a bush),
-//             W2 scalars and view mask.  The scan of _get_nearest_things (:763-810) keeps the
-//             top two of the set cells under (distance ascending, np.where index descending)
-//             (a later cell at equal distance replaces the nearest, :782-791), so the nearest
-//             is the highest set bit of the first non-empty ring and the second the next bit
-//             of that ring or the highest of the next non-empty one; counts are popcounts
+//             W2 scalars and view mask
 //   phase 3   feature bits -> float32, 16-byte stores
-struct FeatLds {
-  uint32_t* in;     // 64 envs x OB bits (+ 4 dwords of slack)
-  uint32_t* ob;     // 64 envs x F bits (+ 4 dwords of slack)
-  uint32_t* enc;    // [128] per cell: up | right << 8 | down << 16 | left << 24 (encoded values)
-  uint4* ring;      // [md] cells at distance d
-  uint4* cmask;     // [4] cells counted up, right, down, left (:812-824)
-};
-
 __device__ __forceinline__ uint32_t feat_in_words(const FeatParams& p) { return ((uint32_t)(64 * p.OB + 31) >> 5) + 4u; }
 __device__ __forceinline__ uint32_t feat_ob_words(const FeatParams& p) { return ((uint32_t)(64 * p.F + 31) >> 5) + 4u; }
 
-__device__ __forceinline__ FeatLds feat_lds(uint32_t* lds, const FeatParams& p) {
-  FeatLds s;
-  const uint32_t a = (feat_in_words(p) + 3u) & ~3u, b = (feat_ob_words(p) + 3u) & ~3u;
-  s.in = lds;
-  s.ob = lds + a;
-  s.enc = lds + a + b;
-  s.ring = reinterpret_cast<uint4*>(lds + a + b + 128);
-  s.cmask = s.ring + p.md;
-  return s;
-}
-
-// bits [at, at + n) of an LDS bit-stream (n <= 128) as a 128-bit mask
-__device__ __forceinline__ M128 stream_get128(const uint32_t* s, uint32_t at, uint32_t n) {
-  const uint32_t* d = s + (at >> 5);
-  const uint32_t sh = at & 31u;
-  const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4];
-  M128 m = m_make(__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
-                  __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh));
-  if (n < 128u) {
-    if (n >= 64u) m.hi &= (1ull << (n - 64u)) - 1ull;
-    else { m.hi = 0ull; m.lo &= (1ull << n) - 1ull; }
-  }
-  return m;
-}
-
-__device__ __forceinline__ int m_top(const M128& m) {
-  return m.hi ? 127 - (int)__clzll((long long)m.hi) : (m.lo ? 63 - (int)__clzll((long long)m.lo) : -1);
-}
-__device__ __forceinline__ M128 m_of(const uint4& v) { return m_make(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ int m_popc(const M128& m) { return __popcll(m.lo) + __popcll(m.hi); }
-
-// nearest / second nearest (packed encodings) and the capped direction counts of plane P
-__device__ __forceinline__ void plane_features(const FeatLds& s, int md, M128 P, uint32_t& near, uint32_t& second,
-                                               int counts[4]) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) counts[k] = min(m_popc(m_and(P, m_of(s.cmask[k]))), 10);
-  int n1 = -1, n2 = -1;
-  for (int d = 0; d < md; ++d) {
-    if (__all(n2 >= 0 || (P.lo | P.hi) == 0ull)) break;  // (wave-uniform exit)
-    const M128 r = m_of(s.ring[d]);
-    M128 m = m_and(P, r);
-    P = m_andn(P, r);
-    const int t = m_top(m);
-    if (n1 < 0) {
-      if (t >= 0) {
-        n1 = t;
-        m_clear(m, (uint32_t)t);
-        n2 = m_top(m);
-      }
-    } else if (n2 < 0) {
-      n2 = t;
-    }
-  }
-  near = n1 >= 0 ? s.enc[n1] : 0u;
-  second = n2 >= 0 ? s.enc[n2] : 0u;
-}
-
 __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const FeatLds s = feat_lds(lds, p);
+  const uint32_t a = (feat_in_words(p) + 3u) & ~3u, b = (feat_ob_words(p) + 3u) & ~3u;
+  uint32_t* in = lds;
+  uint32_t* ob = lds + a;
+  const FeatTables t = feat_tables_at(lds + a + b, p.md);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const int n_active = (int)min((int64_t)64, p.B - g0);
@@ -270,7 +202,7 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
   // phase 1 loads first (every one in flight before anything waits), then the scalars
   const uint32_t nbytes = (uint32_t)n_active * (uint32_t)p.OB;
   const uint8_t* src = p.planes + (size_t)g0 * p.OB;
-  constexpr int kLoads = 6;  // 64 * 363 B = 1452 chunks of 16 B <= 6 per thread
+  constexpr int kLoads = 6;  // 64 * 384 B = 1536 chunks of 16 B <= 6 per thread
   uint4 v[kLoads];
   const uint32_t full = nbytes >> 4;
 #pragma unroll
@@ -284,30 +216,12 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
     role = p.role[g];
     status = p.status[g];
   }
-  // prologue: zero the feature bits and the masks, then the tables
-  {
-    const uint32_t a = (feat_in_words(p) + 3u) & ~3u, b = (feat_ob_words(p) + 3u) & ~3u;
-    for (uint32_t i = tid; i < b + 128u + 4u * (md + 4u); i += 256) lds[a + i] = 0u;
-  }
+  // prologue: zero the feature bits and the tables, then build the tables
+  for (uint32_t i = tid; i < b + feat_tables_words(p.md); i += 256) lds[a + i] = 0u;
   __syncthreads();
-  for (uint32_t c = tid; c < WH; c += 256) {
-    const int r = (int)(c / (uint32_t)p.S), col = (int)(c % (uint32_t)p.S);
-    const int rr = r - p.H / 2, rc = col - p.W / 2;  // :779-780
-    const int up = rr < 0 ? -rr : 0, right = rc > 0 ? rc : 0, down = rr > 0 ? rr : 0, left = rc < 0 ? -rc : 0;
-    const int m = p.md;  // encodings :792-808
-    s.enc[c] = (uint32_t)(up ? m - up : 0) | ((uint32_t)(right ? m - right : 0) << 8) |
-               ((uint32_t)(down ? m - down : 0) << 16) | ((uint32_t)(left ? m - left : 0) << 24);
-    const uint32_t bit = 1u << (c & 31u), w = c >> 5;
-    uint32_t* ring = reinterpret_cast<uint32_t*>(s.ring + (abs(rr) + abs(rc)));
-    atomicOr(&ring[w], bit);
-    uint32_t* cm = reinterpret_cast<uint32_t*>(s.cmask);
-    if (r < p.H / 2) atomicOr(&cm[0 * 4 + w], bit);
-    if (col > p.W / 2) atomicOr(&cm[1 * 4 + w], bit);
-    if (r > p.H / 2) atomicOr(&cm[2 * 4 + w], bit);
-    if (col < p.W / 2) atomicOr(&cm[3 * 4 + w], bit);
-  }
+  feat_tables_build(t, p.W, p.H, p.md, tid, 256);
   {  // phase 1: one 16-bit unit per 16 obs bytes
-    uint16_t* in16 = reinterpret_cast<uint16_t*>(s.in);
+    uint16_t* in16 = reinterpret_cast<uint16_t*>(in);
 #pragma unroll
     for (int k = 0; k < kLoads; ++k) {
       const uint32_t u = (uint32_t)tid + 256u * k;
@@ -316,7 +230,7 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
         uint32_t m = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          // byte != 0 -> bit: OR-fold each byte into its low bit
+          // byte != 0 -> its bit 0 (OR-fold within the byte), then the four flags to bits 0..3
           uint32_t x = w[q] | (w[q] >> 4);
           x |= x >> 2;
           x |= x >> 1;
@@ -337,72 +251,38 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
   if (active) {
     const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB;
     const uint32_t at = (uint32_t)lane * (uint32_t)p.F;
-    const uint32_t M1 = md + 1u;
     if (p.kind == 0) {
-      if (wave <= 1) {  // W0 wolves, W1 bushes: near, second, counts
+      if (wave <= 1) {  // W0 wolves, W1 bushes
         uint32_t near, second;
         int counts[4];
-        plane_features(s, p.md, stream_get128(s.in, ebit + (uint32_t)wave * WH, WH), near, second, counts);
-        const uint32_t base = at + (uint32_t)wave * (8u * M1 + 44u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          fset(s.ob, base + (uint32_t)k * M1 + ((near >> (8 * k)) & 0xFFu));
-          fset(s.ob, base + (4u + (uint32_t)k) * M1 + ((second >> (8 * k)) & 0xFFu));
-          fset(s.ob, base + 8u * M1 + 11u * (uint32_t)k + (uint32_t)counts[k]);
-        }
-        if (wave == 1) {  // standing_on_bush = bushes[md//2, md//2] (:742)
-          const uint32_t sb_bit = ebit + WH + (md / 2u) * (uint32_t)p.S + md / 2u;
-          fset(s.ob, at + 16u * M1 + 88u + ((s.in[sb_bit >> 5] >> (sb_bit & 31u)) & 1u));
-        }
+        plane_features(t, p.md, stream_get128(in, ebit + (uint32_t)wave * WH, WH), near, second, counts);
+        emit_plane(ob, at, wave, p.md, near, second, counts);
       } else if (wave == 2) {
-        uint32_t o = at + 16u * M1 + 88u + 2u;
-        fset(s.ob, o + ft);
-        o += (uint32_t)p.turns_empty + 1u;
-        fset(s.ob, o + role);
-        o += 2u;
-        fset(s.ob, o + status);
-        o += 3u;
-        if (p.restrict_view) {  // view_mask of _get_obs (:360-368), 121 bits
-          const uint32_t* vm = p.view121[role == 1u ? 1 : 0];
-          stream_or128(s.ob, o, m_make(vm[0], vm[1], vm[2], vm[3]));
-        }
+        const uint32_t sb_bit = ebit + WH + (md / 2u) * (uint32_t)p.S + md / 2u;  // :742
+        const uint32_t* vm = p.view121[role == 1u ? 1 : 0];
+        emit_scalars(ob, at, p.md, p.turns_empty, (in[sb_bit >> 5] >> (sb_bit & 31u)) & 1u, ft, role, status,
+                     p.restrict_view != 0, m_make(vm[0], vm[1], vm[2], vm[3]));
       }
     } else {  // SuperBasicObservationWrapper: nearest bush in Discrete(md), food, role, status
       if (wave == 1) {
         uint32_t near, second;
         int counts[4];
-        plane_features(s, p.md, stream_get128(s.in, ebit + WH, WH), near, second, counts);
+        plane_features(t, p.md, stream_get128(in, ebit + WH, WH), near, second, counts);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) fset(s.ob, at + (uint32_t)k * md + ((near >> (8 * k)) & 0xFFu));
+        for (int k = 0; k < 4; ++k) fset(ob, at + (uint32_t)k * md + ((near >> (8 * k)) & 0xFFu));
       } else if (wave == 2) {
         uint32_t o = at + 4u * md;
-        fset(s.ob, o + ft);
+        fset(ob, o + ft);
         o += (uint32_t)p.turns_empty + 1u;
-        fset(s.ob, o + role);
+        fset(ob, o + role);
         o += 2u;
-        fset(s.ob, o + status);
+        fset(ob, o + status);
       }
     }
   }
   __syncthreads();
-  // phase 3: bits -> float32, 16-byte stores (F * 64 floats per block, 16-byte aligned)
-  {
-    const uint32_t nf = (uint32_t)n_active * (uint32_t)p.F;
-    float* dst = p.out + (size_t)g0 * p.F;
-    const uint32_t nq = nf >> 2;
-    for (uint32_t u = (uint32_t)tid; u < nq; u += 256u) {
-      const uint32_t q = 4u * u;
-      const uint32_t b = (s.ob[q >> 5] >> (q & 31u)) & 0xFu;
-      float4 f;
-      f.x = (b & 1u) ? 1.0f : 0.0f;
-      f.y = (b & 2u) ? 1.0f : 0.0f;
-      f.z = (b & 4u) ? 1.0f : 0.0f;
-      f.w = (b & 8u) ? 1.0f : 0.0f;
-      reinterpret_cast<float4*>(dst)[u] = f;
-    }
-    for (uint32_t q = 4u * nq + (uint32_t)tid; q < nf; q += 256u)
-      dst[q] = ((s.ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
-  }
+  // phase 3: bits -> float32 (F * 64 floats per block, 16-byte aligned)
+  store_feature_bits(ob, p.out + (size_t)g0 * p.F, (uint32_t)n_active * (uint32_t)p.F, tid, 256);
 }
 
 // actor_critic.finish_episode returns (actor_critic.py:139-143), one thread per env

@@ -94,6 +94,7 @@ struct Params {
   uint8_t* t_food_turns;
   uint8_t* t_role;
   uint8_t* t_status;
+  float* features;     // wab_step_features: PragmaticObsWrapper features [B][F] (else null)
   unsigned long long* stamps;  // diagnostic builds only (-DWAB_STAMPS): [n_blocks][16] s_memrealtime
 };
 
@@ -128,7 +129,8 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) 
 // LDS of the four-wave small-view step (wab_step_small.hip): one 64-env group per
 // workgroup (dwords)
 struct SmallLayout {
-  uint32_t tiles, thr, stream, stream_words, cval, flag, wolfp, kill, bushp, info, spawn, jbm, jwm, jkey, total;
+  uint32_t tiles, thr, stream, stream_words, cval, flag, wolfp, kill, bushp, info, spawn, jbm, jwm, jkey;
+  uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
 };
 
 __host__ __device__ inline SmallLayout small_layout(const Params& p) {
@@ -148,6 +150,16 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.jbm = o; o += 64u * 4u;
   L.jwm = o; o += 64u * 4u;  // (directly after jbm: zeroed together)
   L.jkey = o; o += 2u * 2u * 64u;
+  L.fbits = L.ftab = L.fzero = L.scal = o;
+  if (p.features) {  // fused features: 64 envs x F bits (+ slack), the per-cell tables (zeroed
+                     // together), the envs' scalars
+    const int md = p.W / 2 + p.H / 2 + 1;
+    const uint32_t F = (uint32_t)(16 * (md + 1) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121);
+    L.fbits = o; o += lds_align4(((64u * F + 31u) >> 5) + 4u);
+    L.ftab = o; o += lds_align4(128u + 4u * ((uint32_t)md + 4u));
+    L.fzero = o - L.fbits;
+    L.scal = o; o += 64u;
+  }
   L.total = o;
   return L;
 }

@@ -27,7 +27,7 @@
 // 32 bits equal) are resolved in a separate branch.
 #include <hip/hip_runtime.h>
 
-#include "wab_small.h"
+#include "wab_feat.h"
 
 namespace wab {
 
@@ -259,6 +259,7 @@ struct Lds {
   uint32_t* jbm;    // [job][4] reset bush bitmaps (W1, W3)
   uint32_t* jwm;    // [job][4] reset wolf cells (W1, W3)
   uint32_t* jkey;   // [2][job][2] the new episodes' keys: W1's copy, W3's copy
+  uint32_t* scal;   // [64] fused features: food_turns | role << 8 | status << 16 of the obs
 };
 
 __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
@@ -276,6 +277,7 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   s.jbm = lds + L.jbm;
   s.jwm = lds + L.jwm;
   s.jkey = lds + L.jkey;
+  s.scal = lds + L.scal;
   return s;
 }
 
@@ -343,9 +345,11 @@ __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const
   if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(nbm);
   p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
   p.food[g] = food2;
-  p.food_turns[g] = (uint8_t)(int)ceil(food2 * (double)p.turns_empty);
+  const uint32_t ft2 = (uint32_t)(int)ceil(food2 * (double)p.turns_empty);
+  p.food_turns[g] = (uint8_t)ft2;
   p.role[g] = (uint8_t)role2;
   p.status[g] = 0;
+  if (p.features) s.scal[(int)(g & 63)] = ft2 | ((uint32_t)role2 << 8);
 }
 
 // --------------------------------------------------------------------------- W0: bushes
@@ -506,6 +510,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
       rls[g] = (uint8_t)role;
       sts[g] = (uint8_t)status;
     }
+    if (p.features && !job) s.scal[lane] = (uint32_t)ft | ((uint32_t)role << 8) | ((uint32_t)status << 16);
     if (!job) {
       p.bushmap[g] = m_word<0>(bm);
       if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(bm);
@@ -785,7 +790,12 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
     uint4* z = reinterpret_cast<uint4*>(s.jbm);
     for (int i = lane; i < 2 * 64; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned)
+    uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
+    for (uint32_t i = lane; i < L.fzero / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   lds_barrier();  // B_init
+  if (p.features) feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
   // ring part C
@@ -854,12 +864,47 @@ __device__ __forceinline__ void store_obs(const Params& p, const uint32_t* strea
 #endif
 }
 
+// --------------------------------------------------------------------------- fused features
+// wab_step_features: PragmaticObsWrapper features (wab_feat.h) of the obs this step returns,
+// from the rendered bit-stream (after B2, or B3) and the scalars each env's writer handed over:
+// W0 the wolf plane, W1 the bush plane, W2 the scalars and view mask, one more barrier, then
+// all 256 threads expand the feature bits to float32 (the featurizer's phases 2 and 3).
+__device__ __forceinline__ void step_features(const Params& p, const SmallLayout& L, uint32_t* lds, int wave,
+                                              int lane) {
+  const int md = p.W / 2 + p.H / 2 + 1;
+  const uint32_t F = (uint32_t)pragmatic_dim(md, p.turns_empty), WH = (uint32_t)p.WH;
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
+  const uint32_t* stream = lds + L.stream;
+  uint32_t* ob = lds + L.fbits;
+  if ((uint32_t)lane < n_active && wave < 3) {
+    const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, at = (uint32_t)lane * F;
+    if (wave <= 1) {  // W0 wolves, W1 bushes
+      uint32_t near, second;
+      int counts[4];
+      plane_features(feat_tables_at(lds + L.ftab, md), md, stream_get128(stream, ebit + (uint32_t)wave * WH, WH), near,
+                     second, counts);
+      emit_plane(ob, at, wave, md, near, second, counts);
+    } else {
+      const uint32_t sc = lds[L.scal + lane];
+      const uint32_t role = (sc >> 8) & 0xFFu;
+      const uint32_t sb_bit = ebit + WH + (uint32_t)(md / 2) * (uint32_t)p.S + (uint32_t)(md / 2);  // :742
+      emit_scalars(ob, at, md, p.turns_empty, (stream[sb_bit >> 5] >> (sb_bit & 31u)) & 1u, sc & 0xFFu, role,
+                   sc >> 16, p.restrict_view != 0, view_mask_of(p, (int)role));
+    }
+  }
+  lds_barrier();
+  store_feature_bits(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
+}
+
 }  // namespace
 
-template <int SLOTS, int G>
+// FEAT: wab_step_features (the fused featurizer); without it the feature code folds away
+template <int SLOTS, int G, bool FEAT>
 __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
   Params p = p0;
   specialise_geometry<G>(p);
+  if constexpr (!FEAT) p.features = nullptr;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const SmallLayout L = small_layout(p);
   if ((int64_t)blockIdx.x * 64 >= p.B) return;  // (uniform over the workgroup)
@@ -875,14 +920,21 @@ __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
     draws_wave<G>(p, L, lds, lane);
   else if (wave == 2) wolves_wave<SLOTS, G>(p, L, lds, lane);
   else ring_wave<SLOTS, G>(p, L, lds, lane);
-  store_obs(p, lds + L.stream, threadIdx.x);
+  if (!FEAT || p.planes) store_obs(p, lds + L.stream, threadIdx.x);
+  if constexpr (FEAT) step_features(p, L, lds, wave, lane);
 }
 
-template __global__ void wab_step_small<8, 0>(Params);
-template __global__ void wab_step_small<16, 0>(Params);
-template __global__ void wab_step_small<32, 0>(Params);
-template __global__ void wab_step_small<8, 11>(Params);
-template __global__ void wab_step_small<16, 11>(Params);
-template __global__ void wab_step_small<32, 11>(Params);
+template __global__ void wab_step_small<8, 0, false>(Params);
+template __global__ void wab_step_small<16, 0, false>(Params);
+template __global__ void wab_step_small<32, 0, false>(Params);
+template __global__ void wab_step_small<8, 11, false>(Params);
+template __global__ void wab_step_small<16, 11, false>(Params);
+template __global__ void wab_step_small<32, 11, false>(Params);
+template __global__ void wab_step_small<8, 0, true>(Params);
+template __global__ void wab_step_small<16, 0, true>(Params);
+template __global__ void wab_step_small<32, 0, true>(Params);
+template __global__ void wab_step_small<8, 11, true>(Params);
+template __global__ void wab_step_small<16, 11, true>(Params);
+template __global__ void wab_step_small<32, 11, true>(Params);
 
 }  // namespace wab

@@ -127,8 +127,7 @@ class BatchedWolvesAndBushesEnv:
         self._reset_once = True
         return self._obs_tuple(self._obs)
 
-    def step(self, actions):
-        """Advance every env one step (wab_env.py:250-342)."""
+    def _step_actions(self, actions):
         t = self._torch
         if not self._reset_once:
             raise RuntimeError("call reset() before step()")
@@ -143,6 +142,11 @@ class BatchedWolvesAndBushesEnv:
             a = self._actions
         else:
             a = a.contiguous()
+        return a
+
+    def step(self, actions):
+        """Advance every env one step (wab_env.py:250-342)."""
+        a = self._step_actions(actions)
         term = ctypes.addressof(self._term["struct"]) if self._term is not None else None
         _lib.check(_lib.load().wab_step(self._h, a.data_ptr(), ctypes.addressof(self._obs["struct"]),
                                         self.reward.data_ptr(), self.done.data_ptr(), term,
@@ -151,6 +155,20 @@ class BatchedWolvesAndBushesEnv:
         if self._term is not None:
             info["terminal_obs"] = self._obs_tuple(self._term)
         return self._obs_tuple(self._obs), self.reward, self.done.bool(), info
+
+    def step_features(self, actions, features, store_planes=True):
+        """step() fused with the PragmaticObsWrapper featurizer (wab_step_features): writes the
+        features [B, F] float32 of the returned obs into `features`; reward, done and the obs
+        scalars as step() does.  store_planes=False leaves the obs planes unwritten (the policy
+        of actor_critic.py never sees them)."""
+        a = self._step_actions(actions)
+        o = self._obs["struct"]
+        st = o if store_planes else _lib.WabObs(None, o.food_turns, o.role, o.status)
+        _lib.check(_lib.load().wab_step_features(self._h, a.data_ptr(), ctypes.addressof(st),
+                                                 self.reward.data_ptr(), self.done.data_ptr(),
+                                                 features.data_ptr(), self._stream()),
+                   "wab_step_features")
+        return features, self.reward, self.done.bool()
 
     def rollout(self, actions):
         """T fused steps: actions [T, B] -> (planes [T,B,3,W,S], scalars [T,3,B], reward [T,B],
