@@ -136,18 +136,24 @@ __device__ __forceinline__ void emit_scalars(uint32_t* ob, uint32_t at, int md, 
   if (restrict_view) stream_or128(ob, o, vm);  // view_mask of _get_obs (:360-368), 121 bits
 }
 
-// feature bits [0, n_active * F) -> float32 at out (16-byte aligned), 16-byte stores
+// feature bits [0, nf) -> float32 at out (16-byte aligned), 16-byte stores: thread t writes
+// float4s u = t + nthreads * i (consecutive lanes, consecutive 16 bytes), i.e. the nibbles at
+// bit 4 (t & 7) of dwords (t >> 3) + (nthreads / 8) i: one LDS read and four bit-field
+// extracts and conversions per float4 (nthreads a multiple of 8)
 __device__ __forceinline__ void store_feature_bits(const uint32_t* ob, float* out, uint32_t nf, int tid, int nthreads) {
-  const uint32_t nq = nf >> 2;
-  for (uint32_t u = (uint32_t)tid; u < nq; u += (uint32_t)nthreads) {
-    const uint32_t q = 4u * u;
-    const uint32_t b = (ob[q >> 5] >> (q & 31u)) & 0xFu;
+  const uint32_t nq = nf >> 2, sh = 4u * ((uint32_t)tid & 7u), step = (uint32_t)nthreads >> 3;
+  const uint32_t* src = ob + ((uint32_t)tid >> 3);
+  float4* dst = reinterpret_cast<float4*>(out) + tid;
+  const uint32_t n_i = nq > (uint32_t)tid ? (nq - (uint32_t)tid + (uint32_t)nthreads - 1u) / (uint32_t)nthreads : 0u;
+#pragma unroll 4
+  for (uint32_t i = 0; i < n_i; ++i) {
+    const uint32_t w = src[step * i];
     float4 f;
-    f.x = (b & 1u) ? 1.0f : 0.0f;
-    f.y = (b & 2u) ? 1.0f : 0.0f;
-    f.z = (b & 4u) ? 1.0f : 0.0f;
-    f.w = (b & 8u) ? 1.0f : 0.0f;
-    reinterpret_cast<float4*>(out)[u] = f;
+    f.x = (float)__builtin_amdgcn_ubfe(w, sh, 1u);
+    f.y = (float)__builtin_amdgcn_ubfe(w, sh + 1u, 1u);
+    f.z = (float)__builtin_amdgcn_ubfe(w, sh + 2u, 1u);
+    f.w = (float)__builtin_amdgcn_ubfe(w, sh + 3u, 1u);
+    dst[(size_t)nthreads * i] = f;
   }
   for (uint32_t q = 4u * nq + (uint32_t)tid; q < nf; q += (uint32_t)nthreads)
     out[q] = ((ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
