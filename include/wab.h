@@ -19,7 +19,7 @@
  *   wab_step              <- WolvesAndBushesEnv.step                wab_env.py:250-342
  *   wab_obs               <- _get_obs 7-tuple                        wab_env.py:359-385
  *   wab_rollout           <- the per-step loop of actor_critic.main  actor_critic.py:185-200
- *                            with pre-chosen actions (T fused steps)
+ *                            with pre-chosen actions (T steps)
  *   wab_destroy           <- (gym.Env.close; nothing to free in the reference)
  *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
  *   wab_featurize_superbasic <- SuperBasicObservationWrapper.observation wab_env.py:900-927
@@ -157,7 +157,7 @@ int wab_reset(wab_handle* h, const uint8_t* mask, const wab_obs* obs, void* stre
 int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward,
              uint8_t* done, const wab_obs* terminal, void* stream);
 
-/* T fused steps in one launch (state stays in registers between steps).
+/* T steps, stream-ordered (T step-kernel launches, no host synchronisation).
  * actions [T][B] int8; obs planes [T][B][3][width][plane_stride] and the scalar
  * arrays [T][B] (an obs "sequence"); reward/done [T][B].  Equivalent to T calls of
  * wab_step with terminal = NULL. */
