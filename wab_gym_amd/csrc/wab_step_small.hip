@@ -6,20 +6,21 @@
 // the kernel at batch 4096 takes nearly as long as at 65536 (SQ_WAIT_ANY ~70 % of wave
 // cycles).  What shortens the step is cutting the longest per-env dependency chain.  Each
 // 64-env group (one env per lane) is served by four waves of one 256-thread workgroup, each
-// running an independent part of the step; they meet at four LDS barriers:
+// running an independent part of the step; they meet at LDS barriers:
 //
-//          W0 bushes             W1 draws             W2 wolves             W3 ring
-//   P0     loads, scroll,        entering row/col     despawn, pursuit,     thresholds, the
-//          first log entries     draws                kill; ring part A     ostrich tile value
-//   -- B0 --
-//   P1     rest of the log,      ring part B          ring part C           ring part D
-//          eat, hunger, starve
+//          W0 bushes             W1 draws              W2 wolves             W3 ring
+//   init   state + first eaten-  thresholds -> LDS     wolf slots, header    tile table -> LDS
+//          log loads
+//   -- B_init --
+//   P0     scroll, entering      the ostrich tile's    despawn, pursuit,     ring [6/12, 1)
+//          row/col draws, log,   value (LDS flag),     wolf grid of S, kill,
+//          eat, hunger, starve   ring [0, 5/12)        ring [5/12, 6/12)
 //   -- B1 --
-//   P2     status, reward,       render S             spawns, wolf slots    reset draws of
-//          done, scalars                                                    the done envs
-//   -- B2 --
-//   P3     state stores, new episodes of the done envs
-//   -- B3 --  all: obs bit-stream -> bytes, 16-byte stores
+//   P1     status, reward,       reset draws (cells    spawns, wolf slots,   reset draws (the
+//          done, scalars,        0..63, LDS flag),     header                rest), new episodes
+//          bushes, food          render S
+//   -- B2 --  (B3: terminal obs, W0 copies S out and builds the new episodes)
+//   all: obs bit-stream -> bytes, 16-byte stores
 //
 // Every wave that needs "done" recomputes it from the flags handed over at B1 (starved from
 // W0, killed from W2), so no wave waits for another's bookkeeping.  Draws are batched four
@@ -164,7 +165,9 @@ __device__ __forceinline__ void ring_part(const Params& p, const Head& h, uint32
 }
 
 // the spawn ring split in twelfths (multiples of 4), balanced against each wave's other work
-// before B1: W0 [0, 2/12), W1 [2/12, 4/12), W2 [4/12, 6/12), W3 [6/12, 1)
+// before B1: W1 [0, 5/12), W2 [5/12, 6/12), W3 [6/12, 1); none on W0, the longest chain
+// (A/B at B = 65536, tools/ab.sh: 2/12-4/12-6/12 11.65 us, this split 11.27 us, with W1's
+// reset draws ahead of its render)
 __device__ __forceinline__ int ring_cut(const Params& p, int k) { return min(p.R, ((p.R * k / 12) + 3) & ~3); }
 
 // reset draws (generate_bushes, initialize_wolves) of every job for view cells
@@ -255,7 +258,7 @@ struct Lds {
   uint32_t* kill;   // [64] (W2, P0)
   uint4* bushp;     // [64] bush grid of S (W0, P0)
   uint32_t* info;   // [64] starved | role << 8 | eaten << 16 | emptied << 24 (W0, P0)
-  uint4* spawn;     // [4][64] ring spawn masks (W1, W2, W3, W0)
+  uint4* spawn;     // [3][64] ring spawn masks (W1, W2, W3)
   uint32_t* jbm;    // [job][4] reset bush bitmaps (W1, W3)
   uint32_t* jwm;    // [job][4] reset wolf cells (W1, W3)
   uint32_t* jkey;   // [2][job][2] the new episodes' keys: W1's copy, W3's copy
@@ -478,11 +481,6 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   const bool starved = food <= 0.0;
   if (starved) food = 0.0;
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
-  {  // spawn ring part W0 (the helpers' parts are longer: they start it earlier)
-    M128 spawn = {0ull, 0ull};
-    if (p.wolves_on) ring_part<G>(p, h, b0, b1, 0, ring_cut(p, 2), spawn);
-    s.spawn[192 + lane] = m_pack(spawn);
-  }
   SMALL_STAMP(3);
   lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
 
@@ -583,14 +581,15 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   SMALL_STAMP(11);
   // spawn ring part W1
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 2), ring_cut(p, 4), spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, 0, ring_cut(p, 5), spawn);
   s.spawn[lane] = m_pack(spawn);
   SMALL_STAMP(12);
   lds_barrier();  // B1
-  // render S (:393-444) for the continuing envs (and the done ones when their terminal obs
-  // is asked for)
   const uint32_t info = s.info[lane];
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), s.kill[lane] != 0u);
+  // render S (:393-444) for the continuing envs (and the done ones when their terminal obs
+  // is asked for); needed only at B2, so after the reset draws W3 waits for
+  auto render = [&]() {
   if (h.active && (!job || p.t_planes)) {
     const uint32_t ebit = (uint32_t)lane * OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
     M128 ost = {0ull, 0ull};
@@ -606,6 +605,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
     stream_or128(s.stream, ebit + WH, bp);
     stream_or128(s.stream, ebit + 2 * WH, ost);
   }
+  };
   // the reset draws of the done envs for view cells [0, 64); W3 draws the rest and waits for
   // flag[1] before it builds the new episodes
   const unsigned long long jm = __ballot(job);
@@ -619,6 +619,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(&s.flag[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  render();
   SMALL_STAMP(13);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -721,15 +722,14 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   SMALL_STAMP(17);
   // ring part B
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 4), ring_cut(p, 6), spawn);
+  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 5), ring_cut(p, 6), spawn);
   s.spawn[64 + lane] = m_pack(spawn);
   SMALL_STAMP(18);
   lds_barrier();  // B1: every ring part, the starve flags and the bushes' counts are in
 
   // spawn_wolves (:325-326): new wolves into free slots (outside the view, not in S)
   unsigned long long wolf_of = 0;
-  spawn = m_or(m_or(m_unpack(s.spawn[lane]), m_unpack(s.spawn[64 + lane])),
-               m_or(m_unpack(s.spawn[128 + lane]), m_unpack(s.spawn[192 + lane])));
+  spawn = m_or(m_or(m_unpack(s.spawn[lane]), m_unpack(s.spawn[64 + lane])), m_unpack(s.spawn[128 + lane]));
   if (active && (spawn.lo | spawn.hi)) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
