@@ -22,6 +22,10 @@ def __getattr__(name):
         from . import egocentric
 
         return getattr(egocentric, name)
+    if name == "EpisodeMonitor":
+        from .monitor import EpisodeMonitor
+
+        return EpisodeMonitor
     if name == "PragmaticObsWrapper":
         from .wrappers import PragmaticObsWrapper
 
