@@ -119,10 +119,18 @@ def main():
     from wab_gym_amd.shard import env_id_base, max_over_ranks, rank_info
 
     rank, world, local = rank_info()
+    # WAB_DIST_BACKEND=gloo rehearses the N > 1 path with every rank on the visible GPUs
+    # (ranks share a GPU when there are fewer GPUs than ranks); the driver's runs use RCCL
+    backend = os.environ.get("WAB_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from wab_gym_amd import _lib
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
