@@ -363,6 +363,35 @@ def test_step_features_matches_step_then_featurize(opts, kw):
     assert ca == cb
 
 
+def test_step_features_argument_errors():
+    import ctypes
+
+    import torch
+
+    from wab_gym_amd import _lib
+
+    env = _env(None, 256)
+    env.reset()
+    L = _lib.load()
+    F = int(L.wab_feature_dim(env._h))
+    feats = torch.zeros(256 * F + 8, device="cuda:0")
+    a = torch.zeros(256, dtype=torch.int8, device="cuda:0")
+    o = env._obs["struct"]
+    s = env._stream()
+    args = lambda f, obs=o: (env._h, a.data_ptr(), ctypes.addressof(obs), env.reward.data_ptr(),  # noqa: E731
+                             env.done.data_ptr(), f, s)
+    assert L.wab_step_features(*args(feats.data_ptr() + 4)) == -1  # features not 16-byte aligned
+    assert b"aligned" in L.wab_last_error()
+    assert L.wab_step_features(*args(None)) == -1
+    bad = _lib.WabObs(o.planes, None, o.role, o.status)
+    assert L.wab_step_features(*args(feats.data_ptr(), bad)) == -1
+    assert L.wab_step_features(*args(feats.data_ptr())) == 0
+    torch.cuda.synchronize()
+    fresh = _env(None, 256)  # no reset yet
+    assert L.wab_step_features(fresh._h, a.data_ptr(), ctypes.addressof(fresh._obs["struct"]),
+                               fresh.reward.data_ptr(), fresh.done.data_ptr(), feats.data_ptr(), s) == -4
+
+
 def test_step_features_keeps_planes_when_asked():
     import torch
 
