@@ -131,11 +131,24 @@ class BatchedWolvesAndBushesEnv:
         t = self._torch
         if not self._reset_once:
             raise RuntimeError("call reset() before step()")
-        a = t.as_tensor(actions, device=self.device)
-        if a.shape != (self.num_envs,):
-            raise ValueError("actions must have shape [num_envs]")
-        if self.validate_actions:
-            if bool(((a < 0) | (a >= self.n_actions)).any()):
+        if not isinstance(actions, t.Tensor):
+            # host actions: checked on the host before the copy (no device synchronisation)
+            import numpy as np
+
+            h = np.asarray(actions)
+            if h.shape != (self.num_envs,):
+                raise ValueError("actions must have shape [num_envs]")
+            if self.validate_actions and h.size and (h.min() < 0 or h.max() >= self.n_actions):
+                raise IndexError("action out of range [0, %d)" % self.n_actions)
+            a = t.as_tensor(h.astype(np.int8, copy=False), device=self.device)
+        else:
+            a = actions.to(self.device)
+            if a.shape != (self.num_envs,):
+                raise ValueError("actions must have shape [num_envs]")
+            # device actions: one synchronising check (validate_actions=False keeps step()
+            # asynchronous; the kernel then counts out-of-range actions as no-ops,
+            # counters()["bad_actions"])
+            if self.validate_actions and bool(((a < 0) | (a >= self.n_actions)).any()):
                 raise IndexError("action out of range [0, %d)" % self.n_actions)
         if a.dtype != t.int8:
             self._actions.copy_(a)
@@ -145,7 +158,8 @@ class BatchedWolvesAndBushesEnv:
         return a
 
     def step(self, actions):
-        """Advance every env one step (wab_env.py:250-342)."""
+        """Advance every env one step (wab_env.py:250-342).  The returned obs, reward and done
+        are views of the env's buffers, overwritten by the next step (clone to keep them)."""
         a = self._step_actions(actions)
         term = ctypes.addressof(self._term["struct"]) if self._term is not None else None
         _lib.check(_lib.load().wab_step(self._h, a.data_ptr(), ctypes.addressof(self._obs["struct"]),
@@ -154,7 +168,7 @@ class BatchedWolvesAndBushesEnv:
         info = {}
         if self._term is not None:
             info["terminal_obs"] = self._obs_tuple(self._term)
-        return self._obs_tuple(self._obs), self.reward, self.done.bool(), info
+        return self._obs_tuple(self._obs), self.reward, self.done.view(self._torch.bool), info
 
     def step_features(self, actions, features, store_planes=True):
         """step() fused with the PragmaticObsWrapper featurizer (wab_step_features): writes the
@@ -168,7 +182,7 @@ class BatchedWolvesAndBushesEnv:
                                                  self.reward.data_ptr(), self.done.data_ptr(),
                                                  features.data_ptr(), self._stream()),
                    "wab_step_features")
-        return features, self.reward, self.done.bool()
+        return features, self.reward, self.done.view(self._torch.bool)
 
     def rollout(self, actions):
         """T fused steps: actions [T, B] -> (planes [T,B,3,W,S], scalars [T,3,B], reward [T,B],
