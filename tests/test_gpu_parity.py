@@ -363,6 +363,37 @@ def test_step_features_matches_step_then_featurize(opts, kw):
     assert ca == cb
 
 
+def test_step_features_full_size_c5():
+    """C5 at its full size (B = 65536): the fused launch (planes not stored) == wab_step +
+    wab_featurize on a twin env for 40 steps; every row one-hot per group (each Discrete block
+    of the flattened 11-tuple holds exactly one 1)."""
+    import torch
+
+    from wab_gym_amd.wrappers import PragmaticObsWrapper
+
+    B = 65536
+    ea, eb = _env(None, B, validate_actions=False), _env(None, B, validate_actions=False)
+    wa, wb = PragmaticObsWrapper(ea), PragmaticObsWrapper(eb)
+    wa.reset()
+    wb.reset()
+    fa = torch.empty((B, wa.feature_dim), device="cuda:0")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(5)
+    md = 11
+    sizes = [md + 1] * 8 + [11] * 4 + [md + 1] * 8 + [11] * 4 + [2, 41, 2, 3]
+    for t in range(40):
+        a = torch.randint(0, 5, (B,), device="cuda:0", generator=g)
+        ea.step_features(a, fa, store_planes=False)
+        eb.step(a)
+        assert torch.equal(fa, wb.observation()), t
+    o = 0
+    for n in sizes:  # the last step's rows
+        assert bool((fa[:, o:o + n].sum(1) == 1).all()), o
+        o += n
+    assert bool((fa[:, o:] == 0).all())  # view mask: zeros without restrict_view
+    assert ea.counters() == eb.counters()
+
+
 def test_step_features_argument_errors():
     import ctypes
 
