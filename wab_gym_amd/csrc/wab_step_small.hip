@@ -1,10 +1,11 @@
 // wab_step_small.hip — the fused step for small views (W*H <= 128 bits, S == H, spawn ring
 // <= 128 tiles; the default 11x11 options).
 //
-// The step is latency-bound, not throughput-bound: a lone wave issues at best one instruction
-// every ~4-5 cycles (twice that along a dependent chain; tools/micro/valu_latency.hip), and
-// the kernel at batch 4096 takes nearly as long as at 65536 (SQ_WAIT_ANY ~70 % of wave
-// cycles).  What shortens the step is cutting the longest per-env dependency chain.  Each
+// The step is bound by its per-env dependency chain and by VALU issue: a lone wave issues at
+// best one instruction every ~4-5 cycles (twice that along a dependent chain;
+// tools/micro/valu_latency.hip), the kernel at batch 4096 takes nearly as long as at 65536,
+// and at 65536 (four waves per SIMD) the VALU pipe is busy about half of a workgroup's life,
+// the rest being load latency and barrier waits (profiles/r01_small).  Each
 // 64-env group (one env per lane) is served by four waves of one 256-thread workgroup, each
 // running an independent part of the step; they meet at LDS barriers:
 //
@@ -21,6 +22,10 @@
 //          bushes, food          render S
 //   -- B2 --  (B3: terminal obs, W0 copies S out and builds the new episodes)
 //   all: obs bit-stream -> bytes, 16-byte stores
+//
+// FEAT (wab_step_features): W1 and W3 also store the all-zero view-mask lines of the feature
+// rows right after B_init; after B2 W0-W2 compute the features from the bit-stream, one more
+// barrier, and all threads store the float32 rows (the planes only if asked for).
 //
 // Every wave that needs "done" recomputes it from the flags handed over at B1 (starved from
 // W0, killed from W2), so no wave waits for another's bookkeeping.  Draws are batched four
