@@ -159,4 +159,78 @@ __device__ __forceinline__ void store_feature_bits(const uint32_t* ob, float* ou
     out[q] = ((ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
 }
 
+// ---- the view-mask lines.  Without restrict_view the view-mask block (the last 121 floats of
+// a row) is all zeros whatever the obs: the whole 128-byte lines inside those blocks (~20 % of
+// the row bytes) can be stored before anything is computed, and the final store skips them.
+// Only whole lines: a line written in two parts at different times costs far more than its
+// bytes (measured).
+struct ViewLines {
+  uint32_t delta;  // the group's first float modulo 128 bytes (line-space origin)
+  uint32_t F;      // floats per row
+  uint32_t vb;     // first byte of the view block within a row
+};
+
+__device__ __forceinline__ ViewLines view_lines(const float* out, uint32_t F) {
+  ViewLines v;
+  v.delta = (uint32_t)reinterpret_cast<uintptr_t>(out) & 127u;
+  v.F = F;
+  v.vb = 4u * (F - 121u);
+  return v;
+}
+
+// the whole lines [first, end) (line space) inside row e's view block
+__device__ __forceinline__ void row_view_lines(const ViewLines& v, uint32_t e, uint32_t& first, uint32_t& end) {
+  const uint32_t row = v.delta + 4u * v.F * e;
+  first = (row + v.vb + 127u) >> 7;
+  end = (row + 4u * v.F) >> 7;
+}
+
+// zeros to the whole view-block lines of rows [e0, e0 + n_rows) of the group at out
+__device__ __forceinline__ void view_zero_lines(float* out, uint32_t F, uint32_t e0, uint32_t n_rows, int t, int nt) {
+  const ViewLines v = view_lines(out, F);
+  constexpr uint32_t kPer = 32;  // chunk slots per row: <= 3 whole lines of 8 chunks in 484 bytes
+  for (uint32_t u = (uint32_t)t; u < n_rows * kPer; u += (uint32_t)nt) {
+    const uint32_t e = e0 + u / kPer, c = u % kPer;
+    uint32_t first, end;
+    row_view_lines(v, e, first, end);
+    if (first * 8u + c < end * 8u)
+      *reinterpret_cast<float4*>(reinterpret_cast<char*>(out) + (first * 128u + 16u * c - v.delta)) =
+          make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
+// store_feature_bits without the chunks in the whole view-block lines (view_zero_lines)
+__device__ __forceinline__ void store_rows_skip_views(const uint32_t* ob, float* out, uint32_t nf, uint32_t F, int tid,
+                                                      int nthreads) {
+  const ViewLines v = view_lines(out, F);
+  const uint32_t nq = nf >> 2, sh = 4u * ((uint32_t)tid & 7u), step = (uint32_t)nthreads >> 3;
+  const uint32_t* src = ob + ((uint32_t)tid >> 3);
+  // chunk u = tid + nthreads i starts at float 4u = e F + r (row e, offset r)
+  uint32_t e = (4u * (uint32_t)tid) / F, r = 4u * (uint32_t)tid - e * F;
+  const uint32_t adv = 4u * (uint32_t)nthreads, dq = adv / F, dr = adv - dq * F;
+#pragma unroll 4
+  for (uint32_t i = 0, u = (uint32_t)tid; u < nq; ++i, u += (uint32_t)nthreads) {
+    uint32_t first, end;
+    row_view_lines(v, e, first, end);
+    const uint32_t line = (v.delta + 16u * u) >> 7;
+    if (line < first || line >= end) {
+      const uint32_t w = src[step * i];
+      float4 f;
+      f.x = (float)__builtin_amdgcn_ubfe(w, sh, 1u);
+      f.y = (float)__builtin_amdgcn_ubfe(w, sh + 1u, 1u);
+      f.z = (float)__builtin_amdgcn_ubfe(w, sh + 2u, 1u);
+      f.w = (float)__builtin_amdgcn_ubfe(w, sh + 3u, 1u);
+      reinterpret_cast<float4*>(out)[u] = f;
+    }
+    e += dq;
+    r += dr;
+    if (r >= F) {
+      r -= F;
+      e += 1u;
+    }
+  }
+  for (uint32_t q = 4u * nq + (uint32_t)tid; q < nf; q += (uint32_t)nthreads)
+    out[q] = ((ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
+}
+
 }  // namespace wab

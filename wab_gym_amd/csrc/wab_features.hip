@@ -182,7 +182,9 @@ __global__ __launch_bounds__(256) void wab_featurize_kernel(FeatParams p) {
 //   phase 1   16-byte loads, 16 bytes -> one 16-bit LDS store (no zeroing, no atomics)
 //   phase 2   lane = env, one plane per wave: W0 wolves, W1 bushes (+ standing on a bush),
 //             W2 scalars and view mask
-//   phase 3   feature bits -> float32, 16-byte stores
+//   phase 3   feature bits -> float32, 16-byte stores (without restrict_view, the whole lines
+//             of the all-zero view-mask blocks go out first, while the phase-1 loads are in
+//             flight, and phase 3 skips them)
 __device__ __forceinline__ uint32_t feat_in_words(const FeatParams& p) { return ((uint32_t)(64 * p.OB + 31) >> 5) + 4u; }
 __device__ __forceinline__ uint32_t feat_ob_words(const FeatParams& p) { return ((uint32_t)(64 * p.F + 31) >> 5) + 4u; }
 
@@ -216,6 +218,10 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
     role = p.role[g];
     status = p.status[g];
   }
+  // while the loads are in flight (issued after them, so no wait on a load waits for these):
+  // the all-zero view-mask lines of the rows (wab_feat.h)
+  const bool zero_views = p.kind == 0 && !p.restrict_view;
+  if (zero_views) view_zero_lines(p.out + (size_t)g0 * p.F, (uint32_t)p.F, 0u, (uint32_t)n_active, tid, 256);
   // prologue: zero the feature bits and the tables, then build the tables
   for (uint32_t i = tid; i < b + feat_tables_words(p.md); i += 256) lds[a + i] = 0u;
   __syncthreads();
@@ -282,7 +288,10 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
   }
   __syncthreads();
   // phase 3: bits -> float32 (F * 64 floats per block, 16-byte aligned)
-  store_feature_bits(ob, p.out + (size_t)g0 * p.F, (uint32_t)n_active * (uint32_t)p.F, tid, 256);
+  if (zero_views)
+    store_rows_skip_views(ob, p.out + (size_t)g0 * p.F, (uint32_t)n_active * (uint32_t)p.F, (uint32_t)p.F, tid, 256);
+  else
+    store_feature_bits(ob, p.out + (size_t)g0 * p.F, (uint32_t)n_active * (uint32_t)p.F, tid, 256);
 }
 
 // actor_critic.finish_episode returns (actor_critic.py:139-143), one thread per env

@@ -361,79 +361,13 @@ __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const
 }
 
 // --------------------------------------------------------------------------- fused features: early lines
-// The view-mask blocks (the last 121 floats of each row) are all zeros without restrict_view,
-// known before the step has computed anything: the whole 128-byte lines inside them (~20 % of
-// the row bytes) are stored right after B_init by W1 (rows 0..31) and W3 (rows 32..63), while
-// the HBM is otherwise idle, and the final store skips them.  Only whole lines: a line written
-// in two parts at different times costs far more than its bytes.
-struct ViewLines {
-  uint32_t delta;  // the group's feature base modulo 128 (line-space origin)
-  uint32_t F;      // floats per row
-  uint32_t vb;     // first byte of the view block within a row
-};
-
-__device__ __forceinline__ ViewLines view_lines(const Params& p, const float* out) {
-  ViewLines v;
-  v.delta = (uint32_t)reinterpret_cast<uintptr_t>(out) & 127u;
-  v.F = (uint32_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
-  v.vb = 4u * (v.F - 121u);
-  return v;
-}
-
-// the whole lines [first, end) (line space) inside row e's view block
-__device__ __forceinline__ void row_view_lines(const ViewLines& v, uint32_t e, uint32_t& first, uint32_t& end) {
-  const uint32_t row = v.delta + 4u * v.F * e;
-  first = (row + v.vb + 127u) >> 7;
-  end = (row + 4u * v.F) >> 7;
-}
-
+// The view-mask blocks of the feature rows are all zeros without restrict_view, known before
+// the step has computed anything: the whole 128-byte lines inside them (wab_feat.h) are stored
+// right after B_init by W1 (rows 0..31) and W3 (rows 32..63), while the HBM is otherwise idle,
+// and the final store skips them.
 __device__ __forceinline__ void early_view_zeros(const Params& p, uint32_t e0, uint32_t n_rows, int lane) {
-  float* out = p.features + (size_t)blockIdx.x * 64u * (size_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
-  const ViewLines v = view_lines(p, out);
-  constexpr uint32_t kPer = 32;  // chunk slots per row: <= 3 whole lines of 8 chunks in 484 bytes
-  for (uint32_t u = (uint32_t)lane; u < n_rows * kPer; u += 64u) {
-    const uint32_t e = e0 + u / kPer, c = u % kPer;
-    uint32_t first, end;
-    row_view_lines(v, e, first, end);
-    if (first * 8u + c < end * 8u)
-      *reinterpret_cast<float4*>(reinterpret_cast<char*>(out) + (first * 128u + 16u * c - v.delta)) =
-          make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-}
-
-// the final store: feature bits [0, nf) -> float32 (as store_feature_bits), without the chunks
-// in the whole view-block lines early_view_zeros wrote
-__device__ __forceinline__ void store_rows_skip_views(const Params& p, const uint32_t* ob, float* out, uint32_t nf,
-                                                      int tid) {
-  const ViewLines v = view_lines(p, out);
-  const uint32_t nq = nf >> 2, sh = 4u * ((uint32_t)tid & 7u);
-  const uint32_t* src = ob + ((uint32_t)tid >> 3);
-  // chunk u = tid + 256 i starts at float 4u = e F + r (row e, offset r), advanced by 1024 floats
-  uint32_t e = (4u * (uint32_t)tid) / v.F, r = 4u * (uint32_t)tid - e * v.F;
-  const uint32_t dq = 1024u / v.F, dr = 1024u - dq * v.F;
-#pragma unroll 4
-  for (uint32_t i = 0, u = (uint32_t)tid; u < nq; ++i, u += 256u) {
-    uint32_t first, end;
-    row_view_lines(v, e, first, end);
-    const uint32_t line = (v.delta + 16u * u) >> 7;
-    if (line < first || line >= end) {
-      const uint32_t w = src[32u * i];
-      float4 f;
-      f.x = (float)__builtin_amdgcn_ubfe(w, sh, 1u);
-      f.y = (float)__builtin_amdgcn_ubfe(w, sh + 1u, 1u);
-      f.z = (float)__builtin_amdgcn_ubfe(w, sh + 2u, 1u);
-      f.w = (float)__builtin_amdgcn_ubfe(w, sh + 3u, 1u);
-      reinterpret_cast<float4*>(out)[u] = f;
-    }
-    e += dq;
-    r += dr;
-    if (r >= v.F) {
-      r -= v.F;
-      e += 1u;
-    }
-  }
-  for (uint32_t q = 4u * nq + (uint32_t)tid; q < nf; q += 256u)
-    out[q] = ((ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
+  const uint32_t F = (uint32_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
+  view_zero_lines(p.features + (size_t)blockIdx.x * 64u * F, F, e0, n_rows, lane, 64);
 }
 
 // --------------------------------------------------------------------------- W0: bushes
@@ -982,7 +916,7 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   }
   lds_barrier();
   if (p.restrict_view) store_feature_bits(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
-  else store_rows_skip_views(p, ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x);
+  else store_rows_skip_views(ob, p.features + (size_t)g0 * F, n_active * F, F, (int)threadIdx.x, 256);
 }
 
 }  // namespace
