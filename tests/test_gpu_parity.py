@@ -212,6 +212,38 @@ def test_rollout_equals_step_loop():
         assert torch.equal(scal[t], e2._obs["scalars"])
 
 
+@pytest.mark.parametrize("opts,kw", [
+    (None, {}),
+    ({"width": 9, "height": 9}, {"wolf_slots": 32}),                 # runtime geometry (G = 0)
+    ({"restrict_view": True, "lookout_only": False}, {"wolf_slots": 16}),
+    (None, {"autoreset": False}),
+    ({"starting_food": None, "starting_role": None}, {}),
+])
+def test_rollout_variants_equal_step_loop(opts, kw):
+    """wab_rollout == T wab_step calls, bit for bit, over two consecutive rollouts (state carried
+    across calls), a partial last group included; final hidden state and counters equal too."""
+    import torch
+
+    B, T = 1008, 60  # 15 full groups + 48 envs; B * 363 obs bytes keeps every step 16-byte aligned
+    rs = np.random.RandomState(9)
+    e1, e2 = _env(opts, B, validate_actions=False, **kw), _env(opts, B, validate_actions=False, **kw)
+    assert e1.step_kernel == "small"
+    e1.reset()
+    e2.reset()
+    for seg in range(2):
+        a = torch.as_tensor(rs.randint(e1.n_actions, size=(T, B)))
+        planes, scal, rew, done = e1.rollout(a)
+        for t in range(T):
+            obs, r, d, _ = e2.step(a[t])
+            assert torch.equal(planes[t], e2._obs["planes"]), (seg, t)
+            assert torch.equal(scal[t], e2._obs["scalars"]), (seg, t)
+            assert torch.equal(rew[t], r) and torch.equal(done[t].bool(), d), (seg, t)
+    s1, s2 = e1.state(), e2.state()
+    for k in s1:
+        assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
+    assert e1.counters() == e2.counters()
+
+
 def test_full_size_properties():
     """B = 65536 over 200 steps: invariants that hold regardless of the trajectory."""
     import torch
