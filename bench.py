@@ -283,21 +283,20 @@ def main():
                        "featurize_us": round(feat_ms * 1e3, 3), "returns_us_per_segment": round(ret_ms * 1e3, 3),
                        "alg_bytes_per_env_step": alg + feat_alg + RETURNS_ALG_BYTES,
                        "achieved_GBs_whole_step": round((alg + feat_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
-        if fused:
-            pass
-        elif feat_ms > step_ms:  # the dominant kernel carries the roofline object
-            fk = ("wab_featurize_small_kernel" if env.W * env.H <= 128 and env.S == env.H
-                  else "wab_featurize_kernel")
-            kernel_name, alg, kern_ms = fk + " (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
-        else:
-            kern_ms = step_ms
+            if feat_ms > step_ms:  # the dominant kernel carries the roofline object
+                fk = ("wab_featurize_small_kernel" if env.W * env.H <= 128 and env.S == env.H
+                      else "wab_featurize_kernel")
+                kernel_name, alg, kern_ms = fk + " (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
+            else:
+                kern_ms = step_ms
     counters = env.counters()
 
     if rank == 0:
         Wv, Hv = env.W, env.H
         achieved = alg * B / (kern_ms * 1e-3) / 1e9
         value = world * B * K / elapsed
-        traffic, traffic_src = committed_traffic(args.config, B)
+        # the committed PMC traffic is of the default launch of each config (C5: the fused one)
+        traffic, traffic_src = committed_traffic(args.config, B) if not args.c5_unfused else (None, None)
         line = {
             "metric": METRIC,
             "value": round(value, 1),
