@@ -9,6 +9,12 @@ kill/eat/starve, reward/done, auto-reset and the full observation render, with t
 owns env ids [rank*B, (rank+1)*B) — independent shards, no collective on the data path
 (weak scaling).  Timing: barrier + synchronize on both sides of exactly K steps, max over
 ranks; value = N*B*K / that time.  Rank 0 prints one JSON line.
+
+Steady state: whatever --warmup asks, at least 2 * max_turns steps run untimed after the
+reset, so the timed window holds the auto-reset mix of the workload (random policy: ~2.4 % of
+the envs finish an episode each step) rather than the first turns of the first episode.
+N > 1: the barrier and the timing MAX go over a CPU (gloo) process group; RCCL is never
+initialised (the shards exchange nothing).
 """
 from __future__ import annotations
 
@@ -65,6 +71,40 @@ def featurize_alg_bytes(W, H, F):
 RETURNS_ALG_BYTES = 9
 
 
+def host_cores():
+    """The host's CPU count (nproc), the cores this process may run on (affinity), the
+    cgroup CPU quota, and the thread count the baseline uses: every core available to the
+    process, capped by the box's CPU share (OMP_NUM_THREADS, which the GPU box sets to its
+    per-GPU share)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    used = aff if quota is None else max(1, min(aff, int(quota)))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if share > 0:
+        used = min(used, share)
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "omp_num_threads": share or None,
+            "used": used}
+
+
+def committed_pmc(config, batch):
+    """VALU figures of the committed PMC summary of this workload's step kernel (SQ counters,
+    tools/profile.sh), or None."""
+    path = os.path.join(REPO, "profiles", "traffic_%s_b%d.json" % (config, batch))
+    if not os.path.exists(path):
+        return None
+    return json.load(open(path)).get("valu")
+
+
 def cpu_baseline(opts, stride, seconds, threads, with_features=False):
     """The C oracle (scalar port of the reference step) timed on this host's cores; for C5 each
     step is followed by the oracle's PragmaticObsWrapper featurizer (one thread)."""
@@ -116,21 +156,15 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from wab_gym_amd.shard import env_id_base, max_over_ranks, rank_info
+    from wab_gym_amd.shard import all_gather_objects, env_id_base, max_over_ranks, rank_info
 
     rank, world, local = rank_info()
-    # WAB_DIST_BACKEND=gloo rehearses the N > 1 path with every rank on the visible GPUs
-    # (ranks share a GPU when there are fewer GPUs than ranks); the driver's runs use RCCL
-    backend = os.environ.get("WAB_DIST_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
+    # ranks share a GPU when there are fewer GPUs than ranks (the 1-GPU rehearsal of N > 1)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")  # CPU only: barrier + timing MAX; no RCCL
 
     from wab_gym_amd import _lib
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
@@ -138,14 +172,16 @@ def main():
     opts, stride, slots, desc = CONFIGS[args.config]
     c5 = args.config == "c5"
     B, K, W = args.batch, args.steps, args.warmup
-    if c5:
-        desc = desc % C5_SEGMENT
-        K = max(C5_SEGMENT, K // C5_SEGMENT * C5_SEGMENT)  # whole segments
-        W = max(C5_SEGMENT, W // C5_SEGMENT * C5_SEGMENT)
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
                                     env_id_base=env_id_base(rank, B),
                                     autoreset=True, validate_actions=False, plane_stride=stride,
                                     wolf_slots=slots)
+    # steady state: at least two full episodes' worth of untimed steps after the reset
+    W = max(W, 2 * int(env.game_options["max_turns"]))
+    if c5:
+        desc = desc % C5_SEGMENT
+        K = max(C5_SEGMENT, K // C5_SEGMENT * C5_SEGMENT)  # whole segments
+        W = max(C5_SEGMENT, -(-W // C5_SEGMENT) * C5_SEGMENT)
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
@@ -211,6 +247,7 @@ def main():
         run(0, W, stream)
         torch.cuda.synchronize(dev)
 
+    c_before = env.counters()  # (synchronises; outside the timed region)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -225,9 +262,13 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed_rank = time.perf_counter() - t0
     stream_ms = ev0.elapsed_time(ev1)
-    elapsed = max_over_ranks(elapsed, dev)
+    elapsed = max_over_ranks(elapsed_rank)
+    c_after = env.counters()
+    window = {"env_steps": c_after["steps"] - c_before["steps"],
+              "resets": c_after["resets"] - c_before["resets"]}
+    window["resets_per_env_step"] = round(window["resets"] / max(1, window["env_steps"]), 5)
 
     # kernel duration: the HIP events around the timed region on the launch stream give the
     # average per launch (back-to-back graph launches: kernel time plus the launch gap, the
@@ -290,10 +331,17 @@ def main():
             else:
                 kern_ms = step_ms
     counters = env.counters()
+    achieved_rank = alg * B / (kern_ms * 1e-3) / 1e9
+    per_rank = all_gather_objects({
+        "rank": rank, "device": str(dev), "env_steps_per_s": round(B * K / elapsed_rank, 1),
+        "ms_per_step": round(elapsed_rank * 1e3 / K, 5), "kernel_us": round(kern_ms * 1e3, 3),
+        "achieved_GBs": round(achieved_rank, 1), "frac": round(achieved_rank / HBM_PEAK_GBS, 4),
+        "timed_window": window, "overflow": counters["wolf_overflow"] + counters["eaten_overflow"],
+        "handoff_timeouts": counters["handoff_timeouts"]})
 
     if rank == 0:
         Wv, Hv = env.W, env.H
-        achieved = alg * B / (kern_ms * 1e-3) / 1e9
+        achieved = achieved_rank
         value = world * B * K / elapsed
         # the committed PMC traffic is of the default launch of each config (C5: the fused one)
         traffic, traffic_src = committed_traffic(args.config, B) if not args.c5_unfused else (None, None)
@@ -303,7 +351,7 @@ def main():
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": W,
+            "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / K, 5),
             "higher_is_better": True,
             "scaling": "weak",
@@ -323,16 +371,25 @@ def main():
                          "kernel_us": round(kern_ms * 1e3, 3),
                          "alg_bytes_per_env_step": alg},
             "stream_us_per_step": round(stream_ms * 1e3 / K, 3),
-            "episodes_finished": counters["resets"],
-            "overflow": {"wolf": counters["wolf_overflow"], "eaten": counters["eaten_overflow"]},
+            "warmup_requested": args.warmup,
+            "warmup_effective": W,
+            "timed_window": window,
+            "overflow": {"wolf": counters["wolf_overflow"], "eaten": counters["eaten_overflow"],
+                         "handoff_timeouts": counters["handoff_timeouts"]},
         }
+        valu = committed_pmc(args.config, B) if not args.c5_unfused else None
+        if valu:
+            line["roofline"]["valu"] = valu
+        if world > 1:
+            line["per_rank"] = per_rank
         if c5:
             line["c5"] = c5_line
         else:
             line["roofline"]["kernel_us_single_launch_median"] = round(single_ms * 1e3, 3)
         if world == 1 and not args.no_cpu:
-            ncpu = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, ncpu, c5)
+            cores = host_cores()
+            line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, cores["used"], c5)
+            line["cpu_baseline"]["host"] = cores
             line["cpu_baseline_1t"] = cpu_baseline(opts, stride, args.cpu_seconds / 2, 1, c5)
         print(json.dumps(line), flush=True)
     if world > 1:

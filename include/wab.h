@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WAB_ABI_VERSION 1
+#define WAB_ABI_VERSION 2
 #define WAB_MAX_WOLF_SLOTS 32 /* largest per-env live-wolf slot count (wab_config.wolf_slots) */
 #define WAB_MAX_VIEW 63       /* largest odd width/height accepted */
 
@@ -116,9 +116,12 @@ typedef struct wab_counters {
   uint64_t wolf_overflow;    /* wolves dropped because all wolf_slots slots were live */
   uint64_t eaten_overflow;   /* eats not logged because the eaten-tile log was full */
   uint64_t bad_actions;      /* actions outside [0, n_actions): treated as no-op */
-  uint64_t steps;            /* env-steps executed */
+  uint64_t steps;            /* env-steps executed: B per step-kernel launch (graph replays
+                              * of captured wab_step calls included) */
   uint64_t resets;           /* env resets executed */
   uint64_t ego_missing;      /* wab_egocentric calls that found a turn of the path unrecorded */
+  uint64_t handoff_timeouts; /* waits on an in-workgroup LDS hand-off that gave up (a hang
+                              * guard; nonzero means results are invalid; must stay 0) */
 } wab_counters;
 
 typedef struct wab_handle wab_handle;

@@ -1,5 +1,6 @@
 """N>1 path on CPU (gloo, world_size 2): shards keyed by global env id reproduce one batch,
-and the timing reduction is a MAX over ranks.  The GPU bench uses the same helpers over RCCL."""
+and the timing reduction is a MAX over ranks.  The GPU bench uses the same helpers over the
+same CPU (gloo) process group: RCCL is never initialised."""
 import os
 import socket
 
@@ -22,7 +23,7 @@ def _worker(rank, world, port, out_dir):
     import torch.distributed as dist
 
     from oracle.oracle import OracleBatch
-    from wab_gym_amd.shard import env_id_base, max_over_ranks
+    from wab_gym_amd.shard import all_gather_objects, env_id_base, max_over_ranks
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -40,6 +41,8 @@ def _worker(rank, world, port, out_dir):
     rg = [torch.zeros(T, B) for _ in range(world)]
     dist.all_gather(rg, torch.as_tensor(np.stack(rewards)))
     tmax = max_over_ranks(1.0 + rank)
+    per_rank = all_gather_objects({"rank": rank, "base": env_id_base(rank, B)})
+    assert per_rank == [{"rank": r, "base": r * B} for r in range(world)]
     if rank == 0:
         np.save(os.path.join(out_dir, "planes.npy"), torch.cat(gathered, dim=1).numpy())
         np.save(os.path.join(out_dir, "reward.npy"), torch.cat(rg, dim=1).numpy())

@@ -38,10 +38,14 @@ def test_gpu_golden_8_slots_and_padded_stride():
 
 # ------------------------------------------------------------------ lockstep vs oracle
 def _lockstep(opts, n, T, autoreset=True, stride=0, threads=16, seed_actions=0, base=0,
-              check_terminal=True, wolf_slots=0):
+              check_terminal=True, wolf_slots=0, return_terminal=True):
+    """The HIP step against the oracle, bit for bit, every step.  return_terminal=False runs
+    the kernels' default auto-reset path (the one bench.py, rollout and step_features use:
+    in the small kernel W3 builds the new episodes after W1's hand-off) instead of the
+    terminal-obs path (W0 builds them after one more barrier)."""
     import torch
 
-    env = _env(opts, n, base, autoreset=autoreset, return_terminal=True, plane_stride=stride,
+    env = _env(opts, n, base, autoreset=autoreset, return_terminal=return_terminal, plane_stride=stride,
                wolf_slots=wolf_slots)
     orc = _oracle(opts, n, base, autoreset, stride)
     obs = env.reset()
@@ -63,7 +67,7 @@ def _lockstep(opts, n, T, autoreset=True, stride=0, threads=16, seed_actions=0, 
         if not np.array_equal(gp, op):
             bad = np.nonzero((gp != op).reshape(n, -1).any(1))[0]
             raise AssertionError("planes differ at t=%d envs %s" % (t, bad[:10]))
-        if autoreset and check_terminal and d.any():
+        if autoreset and check_terminal and return_terminal and d.any():
             tp = env._term["planes"].cpu().numpy()
             assert np.array_equal(tp[d], orc.t_planes[d]), t
             ts = env._term["scalars"].cpu().numpy()
@@ -75,6 +79,7 @@ def _lockstep(opts, n, T, autoreset=True, stride=0, threads=16, seed_actions=0, 
     assert np.array_equal(gs["food"].view(np.uint64), os_["food"].view(np.uint64))
     c = env.counters()
     assert c["wolf_overflow"] == 0 and c["eaten_overflow"] == 0 and c["bad_actions"] == 0
+    assert c["handoff_timeouts"] == 0 and c["steps"] == n * T
     return env, orc
 
 
@@ -83,8 +88,12 @@ def test_c2_batch4096_default_lockstep():
     assert env.counters()["resets"] > 4096  # every env finished at least one episode
 
 
-def test_c3_batch65536_wide31_padded_lockstep():
-    _lockstep({"width": 31, "height": 31}, 65536, 12, stride=32)
+@pytest.mark.parametrize("return_terminal", [False, True])
+def test_c3_batch65536_wide31_padded_lockstep(return_terminal):
+    """C3 at full size with the bench's 16 wolf slots, past the turn-40 starvation (the first
+    mass auto-reset) to desynchronised second episodes."""
+    _lockstep({"width": 31, "height": 31}, 65536, 100, stride=32, wolf_slots=16,
+              return_terminal=return_terminal, seed_actions=3)
 
 
 @pytest.mark.parametrize("opts,stride,slots,autoreset", [
@@ -97,9 +106,11 @@ def test_c3_batch65536_wide31_padded_lockstep():
     ({"width": 13, "height": 11, "turns_to_fill_food": 4, "max_turns": 60, "bush_power": 60}, 16, 8, True),
     ({"width": 31, "height": 31}, 32, 16, False),
 ])
-def test_wide_kernel_lockstep(opts, stride, slots, autoreset):
+@pytest.mark.parametrize("return_terminal", [True, False])
+def test_wide_kernel_lockstep(opts, stride, slots, autoreset, return_terminal):
     """The wide-view kernel (W, H <= 32, rows of 16 or 32 bytes) against the oracle."""
-    env, _ = _lockstep(opts, 1000, 120, autoreset=autoreset, stride=stride, wolf_slots=slots, base=5)
+    env, _ = _lockstep(opts, 1000, 120, autoreset=autoreset, stride=stride, wolf_slots=slots, base=5,
+                       return_terminal=return_terminal)
     assert env.step_kernel == "wide"
 
 
@@ -124,24 +135,73 @@ def test_wide_kernel_reset_mask():
     assert np.array_equal(env.state()["episode"], orc.state()["episode"])
 
 
-def test_headline_batch65536_default_lockstep():
-    _lockstep(None, 65536, 40)
+@pytest.mark.parametrize("return_terminal", [False, True])
+def test_headline_batch65536_default_lockstep(return_terminal):
+    """The headline configuration at full size for 200 steps (> 2 x max_turns): the turn-40
+    mass starvation, the turn-80 cap and the desynchronised later episodes, on both auto-reset
+    paths of the small kernel (return_terminal=False is the bench's)."""
+    env, _ = _lockstep(None, 65536, 200, return_terminal=return_terminal, seed_actions=11)
+    assert env.step_kernel == "small"
+    assert env.counters()["resets"] > 3 * 65536
+
+
+def test_c4_eight_shards_of_65536_match_oracle():
+    """C4 (BASELINE configs[3]) on one GPU: eight 65536-env handles with env_id_base =
+    r * 65536, stepped in turn, against the oracle over all 524288 global env ids, bit for bit,
+    for 100 steps; zero overflow on every shard.  (On 8 GPUs each rank runs exactly one of
+    these handles: bench.py's shards.)"""
+    import torch
+
+    R, B, T = 8, 65536, 100
+    shards = [_env(None, B, r * B, validate_actions=False) for r in range(R)]
+    orc = _oracle(None, R * B)
+    op, of, _, _ = orc.reset()
+    for r, e in enumerate(shards):
+        e.reset()
+        assert np.array_equal(e._obs["planes"].cpu().numpy(), op[r * B:(r + 1) * B]), r
+    rng = np.random.RandomState(2024)
+    for t in range(T):
+        a = rng.randint(5, size=R * B).astype(np.int8)
+        ad = torch.as_tensor(a, device="cuda:0")
+        for r, e in enumerate(shards):
+            e.step(ad[r * B:(r + 1) * B])
+        op, of, orl, ost, orew, odone = orc.step(a, nthreads=16)
+        for r, e in enumerate(shards):
+            sl = slice(r * B, (r + 1) * B)
+            assert np.array_equal(e._obs["planes"].cpu().numpy(), op[sl]), (t, r)
+            assert np.array_equal(e._obs["scalars"].cpu().numpy(), np.stack([of[sl], orl[sl], ost[sl]])), (t, r)
+            assert np.array_equal(e.reward.cpu().numpy(), orew[sl]), (t, r)
+            assert np.array_equal(e.done.cpu().numpy(), odone[sl]), (t, r)
+    os_ = orc.state()
+    for r, e in enumerate(shards):
+        gs = e.state()
+        sl = slice(r * B, (r + 1) * B)
+        for k in ("x", "y", "turn", "n_wolves", "episode"):
+            assert np.array_equal(gs[k], os_[k][sl]), (r, k)
+        assert np.array_equal(gs["food"].view(np.uint64), os_["food"][sl].view(np.uint64)), r
+        c = e.counters()
+        assert c["wolf_overflow"] == 0 and c["eaten_overflow"] == 0 and c["handoff_timeouts"] == 0, (r, c)
+        assert c["steps"] == B * T
 
 
 def test_no_autoreset_keeps_stepping_like_reference():
     _lockstep(None, 2048, 140, autoreset=False)
 
 
-def test_option_variants_lockstep():
+@pytest.mark.parametrize("return_terminal", [True, False])
+def test_option_variants_lockstep(return_terminal):
     for opts in ({"lookout_only": False}, {"restrict_view": True, "lookout_only": False},
                  {"wolves": False}, {"wolves_can_move": False, "god_mode": True},
                  {"starting_food": None, "starting_role": None}, {"width": 9, "height": 13},
-                 {"width": 1, "height": 3}, {"width": 45, "height": 45}):
-        _lockstep(opts, 640, 90, base=77, wolf_slots=32)  # 45x45 exceeds 8 live wolves
+                 {"width": 1, "height": 3}, {"width": 45, "height": 45}, {"wolf_spawn_margin": 2},
+                 {"width": 9, "height": 9}):
+        _lockstep(opts, 640, 90, base=77, wolf_slots=32,  # 45x45 exceeds 8 live wolves
+                  return_terminal=return_terminal)
 
 
-def test_partial_batch_and_large_env_ids():
-    _lockstep(None, 1000, 60, base=2**40 + 5)  # 1000 = 15 full blocks + a 40-env tail
+@pytest.mark.parametrize("return_terminal", [True, False])
+def test_partial_batch_and_large_env_ids(return_terminal):
+    _lockstep(None, 1000, 60, base=2**40 + 5, return_terminal=return_terminal)  # 15 full blocks + a 40-env tail
 
 
 # ------------------------------------------------------------------ surface behaviour
@@ -165,15 +225,50 @@ def test_reset_mask_only_touches_masked_envs():
 
 
 def test_bad_action_raises_and_counts():
+    """Device actions out of range: step() does not synchronise; the kernel applies them as
+    no-ops and counts them, and the next synchronising call raises the IndexError (once).
+    Host actions and validate_actions="sync" raise in step() itself."""
     import torch
 
     env = _env(None, 128)
     env.reset()
+    env.step(torch.full((128,), 5, device="cuda:0"))  # asynchronous
     with pytest.raises(IndexError):
-        env.step(torch.full((128,), 5))
+        env.counters()
+    env.check()  # reported once
+    env.step(torch.full((128,), 2, device="cuda:0"))
+    env.step(torch.full((128,), -3, device="cuda:0", dtype=torch.int8))
+    with pytest.raises(IndexError):
+        env.state()
+    with pytest.raises(IndexError):
+        env.step(np.full(128, 5))  # host actions: checked before the copy
+    env.validate_actions = "sync"
+    with pytest.raises(IndexError):
+        env.step(torch.full((128,), 5, device="cuda:0"))
     env.validate_actions = False
     env.step(torch.full((128,), -1))
-    assert env.counters()["bad_actions"] == 128
+    env.step(torch.full((128,), 261))  # int64 261 must not narrow to the valid action 5
+    env.step(np.full(128, 256))        # nor 256 to 0
+    c = env.counters()
+    assert c["bad_actions"] == 128 * 5
+    assert c["steps"] == 128 * 6 and c["handoff_timeouts"] == 0
+
+
+def test_input_shape_checks():
+    import torch
+
+    from wab_gym_amd.wrappers import PragmaticObsWrapper
+
+    env = _env(None, 256, validate_actions=False)
+    env.reset()
+    with pytest.raises(ValueError):
+        env.rollout(torch.zeros((4, 255), dtype=torch.int8, device="cuda:0"))
+    w = PragmaticObsWrapper(env)
+    with pytest.raises(ValueError):
+        env.step_features(torch.zeros(256, dtype=torch.int8, device="cuda:0"),
+                          torch.zeros((255, w.feature_dim), device="cuda:0"))
+    with pytest.raises(ValueError):
+        w.observation(out=torch.zeros((256, w.feature_dim), dtype=torch.float64, device="cuda:0"))
 
 
 def test_shard_invariance():

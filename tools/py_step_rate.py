@@ -1,5 +1,6 @@
 """Python-level env.step() rate at B = 65536 (drop-in surface, one call per step, device
-actions): validate_actions on (one synchronising check per step) and off (asynchronous)."""
+actions) for each validate_actions mode: True (the default: checked by the kernel, raised at
+the next synchronising call), "sync" (one blocking check per step) and False."""
 import os
 import sys
 import time
@@ -15,7 +16,7 @@ def main():
 
     B, K = 65536, 300
     acts = torch.randint(0, 5, (K, B), device="cuda:0", dtype=torch.int8)
-    for validate in (True, False):
+    for validate in (True, "sync", False):
         env = BatchedWolvesAndBushesEnv(num_envs=B, device="cuda:0", validate_actions=validate)
         env.reset()
         for k in range(20):
@@ -26,8 +27,9 @@ def main():
             env.step(acts[k])
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / K
+        env.check()
         print("env.step validate_actions=%s: %.1f us/step, %.2f G env-steps/s" % (validate, dt * 1e6, B / dt / 1e9))
-    w = PragmaticObsWrapper(BatchedWolvesAndBushesEnv(num_envs=B, device="cuda:0", validate_actions=False))
+    w = PragmaticObsWrapper(BatchedWolvesAndBushesEnv(num_envs=B, device="cuda:0"))
     w.reset()
     for k in range(20):
         w.step(acts[k])

@@ -43,6 +43,22 @@ def main(src, dst, kernel=r"wab_kernel<0|wab_step_q4"):
         w = summ["pmc_mean_per_dispatch"]["WRITE_SIZE"] * 1024.0
         summ["hbm_bytes_per_launch"] = {"fetch_raw": f, "fetch_corrected_x2": 2 * f, "write": w,
                                         "total_corrected": 2 * f + w}
+    m = summ["pmc_mean_per_dispatch"]
+    if "SQ_ACTIVE_INST_VALU" in m and "SQ_WAVES" in m:
+        # SQ_* count quad-cycles summed over the chip (MI355X_MICROARCH.md cycle constants);
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles, so /8 is the launch's cycle count
+        simds = 256 * 4
+        v = {"insts_per_wave": m["SQ_INSTS_VALU"] / m["SQ_WAVES"],
+             "salu_insts_per_wave": m.get("SQ_INSTS_SALU", 0.0) / m["SQ_WAVES"],
+             "active_cycles_per_simd": 4.0 * m["SQ_ACTIVE_INST_VALU"] / simds}
+        if "GRBM_GUI_ACTIVE" in m:
+            cyc = m["GRBM_GUI_ACTIVE"] / 8.0
+            v["launch_cycles"] = cyc
+            v["busy_frac"] = v["active_cycles_per_simd"] / cyc
+            if "trace" in summ:
+                v["clock_GHz"] = cyc / summ["trace"]["avg_ns"]
+        v["source"] = "SQ_INSTS_VALU / SQ_WAVES; busy = 4 * SQ_ACTIVE_INST_VALU / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8)"
+        summ["valu"] = v
     json.dump(summ, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     print(json.dumps(summ, indent=1))
 

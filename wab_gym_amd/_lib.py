@@ -20,7 +20,7 @@ EXPORTED = [
     "wab_debug_bush_values", "wab_step_features",
 ]
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class WabObs(ctypes.Structure):
@@ -31,7 +31,8 @@ class WabObs(ctypes.Structure):
 class WabCounters(ctypes.Structure):
     _fields_ = [("wolf_overflow", ctypes.c_uint64), ("eaten_overflow", ctypes.c_uint64),
                 ("bad_actions", ctypes.c_uint64), ("steps", ctypes.c_uint64),
-                ("resets", ctypes.c_uint64), ("ego_missing", ctypes.c_uint64)]
+                ("resets", ctypes.c_uint64), ("ego_missing", ctypes.c_uint64),
+                ("handoff_timeouts", ctypes.c_uint64)]
 
 
 class WabError(RuntimeError):

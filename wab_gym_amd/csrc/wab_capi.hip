@@ -403,7 +403,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   rc |= alloc((void**)&p.eaten_xy, B * 4 * (size_t)cap);
   rc |= alloc((void**)&p.eaten_rem, B * (size_t)cap);
   rc |= alloc((void**)&p.bushmap, B * 4 * (size_t)(p.W <= 32 && p.WHW < 32 ? 32 : p.WHW));  // (wide: 32 per env)
-  rc |= alloc((void**)&p.counters, 4 * 8);
+  rc |= alloc((void**)&p.counters, wab::kNumCounters * 8);
   rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   uint64_t* thr = nullptr;
   rc |= alloc((void**)&thr, (size_t)(p.max_berries > 0 ? p.max_berries : 1) * 8);
@@ -444,7 +444,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     std::vector<uint4> init(B, make_uint4(0u, 0u, 0u, 0xFFFFFFFFu));
     e = hipMemcpy(p.hdr, init.data(), B * 16, hipMemcpyHostToDevice);
   }
-  if (e == hipSuccess) e = hipMemset(p.counters, 0, 4 * 8);
+  if (e == hipSuccess) e = hipMemset(p.counters, 0, wab::kNumCounters * 8);
   if (e == hipSuccess) e = hipMemset(p.block_resets, 0, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   for (void* k : {kernel_ptr<0, true>(slots), kernel_ptr<1, true>(slots), kernel_ptr<0, false>(slots),
                   kernel_ptr<1, false>(slots)})
@@ -568,17 +568,18 @@ int wab_get_counters(wab_handle* h, wab_counters* out, void* stream) {
   g_err.clear();
   if (!h || !out) return fail(WAB_E_INVALID, "wab_get_counters: NULL argument");
   DeviceGuard guard(h->device);
-  unsigned long long c[4] = {0, 0, 0, 0};
+  unsigned long long c[wab::kNumCounters] = {};
   std::vector<unsigned long long> br((size_t)(h->n_blocks > 0 ? h->n_blocks : 1));
   HIP_TRY(hipMemcpyAsync(c, h->p.counters, sizeof(c), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipMemcpyAsync(br.data(), h->p.block_resets, br.size() * 8, hipMemcpyDeviceToHost,
                          (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-  out->ego_missing = c[3];
-  out->wolf_overflow = c[0];
-  out->eaten_overflow = c[1];
-  out->bad_actions = c[2];
-  out->steps = 0;
+  out->wolf_overflow = c[wab::CTR_WOLF_OVERFLOW];
+  out->eaten_overflow = c[wab::CTR_EATEN_OVERFLOW];
+  out->bad_actions = c[wab::CTR_BAD_ACTIONS];
+  out->ego_missing = c[wab::CTR_EGO_MISSING];
+  out->steps = c[wab::CTR_STEPS];
+  out->handoff_timeouts = c[wab::CTR_HANDOFF_TIMEOUTS];
   out->resets = 0;
   for (size_t i = 0; i < br.size(); ++i) out->resets += br[i];
   return WAB_OK;

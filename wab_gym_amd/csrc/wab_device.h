@@ -205,6 +205,28 @@ __device__ __forceinline__ void decode_action(const Params& p, int a, int& dx, i
 
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
 
+// wab_counters.steps: one lane of workgroup 0 adds the batch size once per step launch (a
+// no-return atomic: nothing waits for it)
+__device__ __forceinline__ void count_steps(const Params& p) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[CTR_STEPS], (unsigned long long)p.B);
+}
+
+// Hand-off of LDS data between two waves of one workgroup through an LDS flag, without a
+// barrier: the producer's release store orders its earlier LDS writes before the flag, the
+// consumer's acquire load its later LDS reads after it.  The producer always makes progress
+// (it is in the same workgroup and waits on nothing), so the bound on the wait is only a hang
+// guard: a wait that gives up is counted (CTR_HANDOFF_TIMEOUTS; the parity tests assert 0).
+__device__ __forceinline__ void lds_publish(uint32_t* flag) {
+  __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_await(const Params& p, const uint32_t* flag) {
+  for (int spin = 0; spin < (1 << 20); ++spin) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  atomicAdd(&p.counters[CTR_HANDOFF_TIMEOUTS], 1ull);
+}
+
 // Workgroup barrier for LDS hand-offs only.  Waves of a block exchange data exclusively
 // through LDS; __syncthreads() would also drain every outstanding global store
 // (s_waitcnt vmcnt(0)) and put HBM write latency on the critical path of each phase.

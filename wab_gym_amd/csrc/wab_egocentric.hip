@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64) void wab_egocentric_kernel(EgoParams p) {
   const bool wave_stale = __any(stale);
   if (lane == 0) {
     if (turn < p.cap) p.path[(size_t)turn * p.B + g] = make_uint4(h.x, live_seen, h.w, 0u);
-    if (wave_stale || turn >= p.cap) atomicAdd(&p.counters[3], 1ull);
+    if (wave_stale || turn >= p.cap) atomicAdd(&p.counters[CTR_EGO_MISSING], 1ull);
   }
 }
 

@@ -12,6 +12,17 @@ constexpr int kEnvsPerBlock = 64;   // env lanes = wave 0 of the block
 constexpr int kThreads = 256;       // 4 waves: waves 0..3 share the tile-parallel phases
 constexpr int kMaxWolfSlots = 32;
 
+// device counters (Params::counters, read back by wab_get_counters; rare events: atomics)
+enum : int {
+  CTR_WOLF_OVERFLOW = 0,
+  CTR_EATEN_OVERFLOW = 1,
+  CTR_BAD_ACTIONS = 2,
+  CTR_EGO_MISSING = 3,
+  CTR_STEPS = 4,             // + B per step launch (one lane of workgroup 0)
+  CTR_HANDOFF_TIMEOUTS = 5,  // bounded LDS hand-off waits that gave up (must stay 0)
+  kNumCounters = 8
+};
+
 // per-env packed misc word: role [0,8) status [8,10) n_wolves [10,16) n_eaten [16,24)
 // n_emptied [24,32) (eaten-log entries with no berries left)
 __host__ __device__ inline uint32_t misc_pack(uint32_t role, uint32_t status, uint32_t nw, uint32_t ne,
@@ -79,7 +90,7 @@ struct Params {
   uint32_t* eaten_xy;  // [cap][B] packed tiles
   uint8_t* eaten_rem;  // [cap][B] berries left
   uint32_t* bushmap;   // [WHW][B] bush presence of the current view, bit i*H + j (post-eat)
-  unsigned long long* counters;      // [3]: wolf_overflow, eaten_overflow, bad_actions (rare: atomics)
+  unsigned long long* counters;      // [kNumCounters] (CTR_*)
   unsigned long long* block_resets;  // [n_blocks]: resets done by each block (owned, no atomics)
   // ---- io (device, caller-owned)
   const int8_t* actions;
@@ -210,7 +221,7 @@ struct EgoParams {
   uint4* path;              // [cap][B] {ostrich tile, food>0 tiles seen so far, episode, 0}
   const uint8_t* mask;      // nullable: only envs with mask[i] != 0
   uint8_t* out;             // [B][5]
-  unsigned long long* counters;  // [3]: path entries missing (stale or beyond cap)
+  unsigned long long* counters;  // [kNumCounters]: CTR_EGO_MISSING, path entries missing (stale or beyond cap)
 };
 
 // wab_featurize / wab_featurize_superbasic (wab_features.hip)

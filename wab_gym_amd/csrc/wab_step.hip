@@ -515,10 +515,11 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
     }
   }
   if (envlane && (bad | eaten_of | wolf_of)) {
-    if (bad) atomicAdd(&p.counters[2], bad);
-    if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
-    if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+    if (bad) atomicAdd(&p.counters[CTR_BAD_ACTIONS], bad);
+    if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
+    if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
   }
+  if constexpr (MODE == MODE_STEP) count_steps(p);
   lds_barrier();
   WAB_STAMP(4);
 
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
           bits &= bits - 1;
           const uint32_t t = tiles[wd * 32 + b];
           if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = xy_pack(tile_dx(t), tile_dy(t));
-          else atomicAdd(&p.counters[0], 1ull);
+          else atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], 1ull);
         }
       }
       p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role, 0u, (uint32_t)n, 0u, 0u), ep);

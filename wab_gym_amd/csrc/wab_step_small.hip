@@ -461,11 +461,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   if (found < 0) {
     rem = 0;
     if (center_bush) {
-      // W1 publishes the values right after B_init; the bound only guards against a hang
-      for (int spin = 0; spin < (1 << 20); ++spin) {
-        if (__hip_atomic_load(s.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
+      lds_await(p, s.flag);  // W1 publishes the values right after B_init
       rem = (int)s.cval[lane];
     }
   }
@@ -532,8 +528,9 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
       p.food[g] = food;
     }
   }
-  if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
-  if (active && !h.valid_action) atomicAdd(&p.counters[2], 1ull);
+  if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
+  if (active && !h.valid_action) atomicAdd(&p.counters[CTR_BAD_ACTIONS], 1ull);
+  count_steps(p);
   const unsigned long long jm = __ballot(job);
   if (lane == 0 && jm) p.block_resets[blockIdx.x] += (unsigned long long)__popcll(jm);
   SMALL_STAMP(4);
@@ -557,7 +554,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
         new_episode<SLOTS>(p, s, h, g, __popcll(jm & ((1ull << lane) - 1ull)), ebit, wolf_of);
       }
     }
-    if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+    if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     lds_barrier();  // B3
   }
   SMALL_STAMP(5);
@@ -590,8 +587,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   // the generated berries of the ostrich's tile (:631-635), for W0
   s.cval[lane] =
       (uint32_t)bush_value_fast(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1), p.bush_power);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_store(s.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  lds_publish(s.flag);  // every lane: each orders its own cval entry
   __builtin_amdgcn_s_setprio(0);
   if (p.features && !p.restrict_view)  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
@@ -633,8 +629,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
       *reinterpret_cast<uint2*>(&s.jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
     }
     reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm, s.jwm);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&s.flag[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_publish(&s.flag[1]);
   }
   render();
   SMALL_STAMP(13);
@@ -779,7 +774,7 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
                           misc_pack((info >> 8) & 0xFFu, status, (uint32_t)n, (info >> 16) & 0xFFu, info >> 24),
                           h.hdr.w);
   }
-  if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+  if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
   SMALL_STAMP(19);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -840,14 +835,10 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
     for (uint32_t c0 = 64; c0 < (uint32_t)p.WH; c0 += 64)  // cells [0, 64): W1
       reset_chunk(p, s.tiles, jkey, n_jobs, c0, lane, s.jbm, s.jwm);
     if (!p.t_planes) {
-      for (int spin = 0; spin < (1 << 20); ++spin) {  // W1's part of the draws (bounded wait)
-        if (__hip_atomic_load(&s.flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_await(p, &s.flag[1]);  // W1's part of the draws
       unsigned long long wolf_of = 0;
       if (job) new_episode<SLOTS>(p, s, h, g, j, (uint32_t)lane * (uint32_t)p.OB, wolf_of);
-      if (wolf_of) atomicAdd(&p.counters[0], wolf_of);
+      if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     }
   }
   SMALL_STAMP(25);

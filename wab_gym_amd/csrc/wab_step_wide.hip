@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
           rls[g] = (uint8_t)h.role;
           sts[g] = (uint8_t)status;
         }
-        if (!h.valid_action) atomicAdd(&p.counters[2], 1ull);
+        if (!h.valid_action) atomicAdd(&p.counters[CTR_BAD_ACTIONS], 1ull);
       }
       info[lane] = (job ? 1u : 0u) | (emptied ? 2u : 0u);
       const unsigned long long jm = __ballot(job);
@@ -660,8 +660,9 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       for (unsigned long long jj = jmask; jj; jj &= jj - 1) obs_env_all(p, bm, wp, tout, (uint32_t)(__ffsll(jj) - 1), tid);
     }
     if (wave == 0) {
-      if (eaten_of) atomicAdd(&p.counters[1], eaten_of);
+      if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
       if (lane == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
+      count_steps(p);
     }
   } else {
     if (tid == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       for (uint32_t i = tid; i < (uint32_t)p.W; i += 256) p.bushmap[(size_t)(g0 + e) * 32u + i] = bm[e * P + i];
     }
   }
-  if (wave == 0 && wolf_of) atomicAdd(&p.counters[0], wolf_of);
+  if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
 #ifdef WAB_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   WIDE_STAMP(8 * wave + 6);

@@ -18,7 +18,11 @@ Differences from the reference, by design (documented in DESIGN.md):
     the same call; `obs` then holds the new episode's first observation and
     `info["terminal_obs"]` (if `return_terminal=True`) the step's own observation;
   * an action outside [0, n_actions) raises IndexError (the reference raises for
-    a >= n via `.iloc` and silently wraps negatives, wab_env.py:253).
+    a >= n via `.iloc` and silently wraps negatives, wab_env.py:253).  Host actions are
+    checked before their copy; device actions are checked by the kernel (the step applies
+    them as no-ops and counts them) and the IndexError is raised by the next synchronising
+    call -- counters(), state() or check() -- so step() never waits for the device
+    (validate_actions="sync" restores an immediate, synchronising check).
 """
 from __future__ import annotations
 
@@ -52,7 +56,10 @@ class BatchedWolvesAndBushesEnv:
         self.env_id_base = int(env_id_base)
         self.autoreset = bool(autoreset)
         self.return_terminal = bool(return_terminal)
-        self.validate_actions = bool(validate_actions)
+        if validate_actions not in (True, False, "sync", "deferred"):
+            raise ValueError("validate_actions must be True/'deferred', 'sync' or False")
+        self.validate_actions = validate_actions
+        self._bad_seen = 0  # bad_actions already reported (deferred validation)
         dev = torch.device(device)
         if dev.type != "cuda":
             raise ValueError("BatchedWolvesAndBushesEnv runs on a HIP device (device='cuda[:i]')")
@@ -140,22 +147,45 @@ class BatchedWolvesAndBushesEnv:
                 raise ValueError("actions must have shape [num_envs]")
             if self.validate_actions and h.size and (h.min() < 0 or h.max() >= self.n_actions):
                 raise IndexError("action out of range [0, %d)" % self.n_actions)
+            if h.dtype != np.int8:  # out-of-range values stay out of range in int8
+                h = np.clip(h, -1, 127)
             a = t.as_tensor(h.astype(np.int8, copy=False), device=self.device)
         else:
             a = actions.to(self.device)
             if a.shape != (self.num_envs,):
                 raise ValueError("actions must have shape [num_envs]")
-            # device actions: one synchronising check (validate_actions=False keeps step()
-            # asynchronous; the kernel then counts out-of-range actions as no-ops,
-            # counters()["bad_actions"])
-            if self.validate_actions and bool(((a < 0) | (a >= self.n_actions)).any()):
+            # device actions: the kernel counts out-of-range actions (applied as no-ops);
+            # validate_actions=True raises at the next synchronising call, "sync" here
+            # (one blocking reduction per step)
+            if self.validate_actions == "sync" and bool(((a < 0) | (a >= self.n_actions)).any()):
                 raise IndexError("action out of range [0, %d)" % self.n_actions)
         if a.dtype != t.int8:
-            self._actions.copy_(a)
+            # narrowing must not wrap an out-of-range value into a valid one (256 -> 0)
+            self._actions.copy_(a.clamp(-1, 127) if not a.is_floating_point() else a.clamp(-1.0, 127.0))
             a = self._actions
         else:
             a = a.contiguous()
         return a
+
+    def _check_features(self, features, F):
+        t = self._torch
+        if (not isinstance(features, t.Tensor) or features.dtype != t.float32 or features.device != self.device
+                or tuple(features.shape) != (self.num_envs, F) or not features.is_contiguous()):
+            raise ValueError("features must be a contiguous float32 tensor of shape (%d, %d) on %s"
+                             % (self.num_envs, F, self.device))
+
+    def _deferred_action_check(self, bad_actions):
+        """Raise the IndexError of out-of-range device actions stepped since the last check
+        (validate_actions=True): they were applied as no-ops, counted by the kernel."""
+        new = bad_actions - self._bad_seen
+        self._bad_seen = bad_actions
+        if self.validate_actions and new > 0:
+            raise IndexError("%d action(s) out of range [0, %d) were stepped since the last check "
+                             "(applied as no-ops)" % (new, self.n_actions))
+
+    def check(self):
+        """Synchronise and raise the deferred IndexError of out-of-range device actions."""
+        self.counters()
 
     def step(self, actions):
         """Advance every env one step (wab_env.py:250-342).  The returned obs, reward and done
@@ -176,6 +206,7 @@ class BatchedWolvesAndBushesEnv:
         scalars as step() does.  store_planes=False leaves the obs planes unwritten (the policy
         of actor_critic.py never sees them)."""
         a = self._step_actions(actions)
+        self._check_features(features, int(_lib.load().wab_feature_dim(self._h)))
         o = self._obs["struct"]
         st = o if store_planes else _lib.WabObs(None, o.food_turns, o.role, o.status)
         _lib.check(_lib.load().wab_step_features(self._h, a.data_ptr(), ctypes.addressof(st),
@@ -188,7 +219,12 @@ class BatchedWolvesAndBushesEnv:
         """T fused steps: actions [T, B] -> (planes [T,B,3,W,S], scalars [T,3,B], reward [T,B],
         done [T,B]).  Equivalent to T step() calls without terminal observations."""
         t = self._torch
-        a = t.as_tensor(actions, device=self.device).to(t.int8).contiguous()
+        a = t.as_tensor(actions, device=self.device)
+        if a.dim() != 2 or a.shape[1] != self.num_envs:
+            raise ValueError("actions must have shape [T, num_envs]")
+        if a.dtype != t.int8:
+            a = a.clamp(-1, 127)
+        a = a.to(t.int8).contiguous()
         T = a.shape[0]
         planes = t.empty((T, self.num_envs, 3, self.W, self.S), dtype=t.uint8, device=self.device)
         scal = t.empty((3, T, self.num_envs), dtype=t.uint8, device=self.device)
@@ -224,7 +260,9 @@ class BatchedWolvesAndBushesEnv:
         c = _lib.WabCounters()
         _lib.check(_lib.load().wab_get_counters(self._h, ctypes.addressof(c), self._stream()),
                    "wab_get_counters")
-        return {k: int(getattr(c, k)) for k, _ in _lib.WabCounters._fields_}
+        out = {k: int(getattr(c, k)) for k, _ in _lib.WabCounters._fields_}
+        self._deferred_action_check(out["bad_actions"])
+        return out
 
     def state(self):
         """Hidden per-env state (host numpy): food f64, x, y, turn, n_wolves, episode."""
@@ -235,6 +273,8 @@ class BatchedWolvesAndBushesEnv:
         P = lambda a: a.ctypes.data  # noqa: E731
         _lib.check(_lib.load().wab_get_state(self._h, P(food), P(x), P(y), P(turn), P(nw), P(ep),
                                              self._stream()), "wab_get_state")
+        if self.validate_actions:
+            self.counters()  # (raises the deferred IndexError, if any)
         return dict(food=food, x=x, y=y, turn=turn, n_wolves=nw, episode=ep)
 
     def seed(self, seed=None):

@@ -60,6 +60,7 @@ class PragmaticObsWrapper:
         if view_mask is not None:
             vm = t.as_tensor(view_mask, device=env.device).to(t.uint8).contiguous()
         dst = self.features if out is None else out
+        env._check_features(dst, self.feature_dim)
         _lib.check(_lib.load().wab_featurize(env._h, ctypes.addressof(st),
                                              None if vm is None else vm.data_ptr(), dst.data_ptr(),
                                              env._stream()), "wab_featurize")
@@ -117,6 +118,7 @@ class SuperBasicObservationWrapper(PragmaticObsWrapper):
                              scal[2].data_ptr())
             keep = (planes, scal)
         dst = self.features if out is None else out
+        env._check_features(dst, self.feature_dim)
         _lib.check(_lib.load().wab_featurize_superbasic(env._h, ctypes.addressof(st), dst.data_ptr(),
                                                         env._stream()), "wab_featurize_superbasic")
         del keep
