@@ -24,7 +24,8 @@
  *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
  *   wab_featurize_superbasic <- SuperBasicObservationWrapper.observation wab_env.py:900-927
  *   wab_step_features        <- PragmaticObsWrapper(env).step, actor_critic.py:180-192
- *   wab_render            <- WolvesAndBushesEnv.render (rgb_array)   wab_env.py:468-502
+ *   wab_render            <- WolvesAndBushesEnv.render (rgb_array,   wab_env.py:468-502
+ *                            draw_health text included)
  *   wab_egocentric        <- WolvesAndBushesEnvEgoCentric._get_obs /  wab_env.py:930-979
  *                            _get_bush_proximities                   wab_env.py:652-667
  *                            + gym.spaces.flatten                    actor_critic.py:188
@@ -216,10 +217,12 @@ int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, 
 int wab_superbasic_dim(const wab_handle* h);
 int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features, void* stream);
 
-/* WolvesAndBushesEnv.render(mode="rgb_array", scale, draw_health=False) (wab_env.py:468-502)
- * of an observation this handle produced: rgb [B][W*scale][H*scale][3] u8 device pointer.
- * The food-count text overlay of draw_health=True (PIL font) is not drawn. */
-int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, void* stream);
+/* WolvesAndBushesEnv.render(mode="rgb_array", scale, draw_health) (wab_env.py:468-502) of an
+ * observation this handle produced: rgb [B][W*scale][H*scale][3] u8 device pointer.  With
+ * draw_health != 0 (the reference's default) the turns-until-starve count (obs->food_turns)
+ * is drawn at (0, 0) in blue with the digit glyphs of PIL's default font (wab_glyphs.h). */
+int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, int32_t draw_health, uint8_t* rgb,
+               void* stream);
 
 /* Bush proximities of the egocentric env variants (WolvesAndBushesEnvEgoCentric and
  * WolvesAndBushesEnvEgocentricJustBushes, wab_env.py:930-979) for the handle's current state:

@@ -24,6 +24,7 @@ def build(quiet=True):
 
 def _stale():
     srcs = [os.path.join(HERE, f) for f in ("wab_oracle.c", "wab_oracle.h", "Makefile")]
+    srcs.append(os.path.join(os.path.dirname(HERE), "wab_gym_amd", "csrc", "wab_glyphs.h"))
     srcs.append(os.path.join(os.path.dirname(HERE), "include", "wab.h"))
     t = os.path.getmtime(LIB_PATH)
     return any(os.path.exists(s) and os.path.getmtime(s) > t for s in srcs)
@@ -52,7 +53,7 @@ def lib():
         L.wabo_featurize.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 6
         L.wabo_egocentric.argtypes = [P, P]
         L.wabo_superbasic_dim.argtypes = [ctypes.c_int] * 3
-        L.wabo_render.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 5 + [P] * 4
+        L.wabo_render.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 6 + [P] * 5
         L.wabo_featurize_superbasic.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 5
         L.wabo_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_double, P, P]
         _lib = L
@@ -165,14 +166,19 @@ def featurize_superbasic(planes, food_turns, role, status, W, H, turns_empty=40)
     return out
 
 
-def render(planes, role, status, W, H, restrict_view=False, scale=32):
-    """render(mode="rgb_array", scale, draw_health=False) of observations -> u8 [B, W*s, H*s, 3]."""
+def render(planes, role, status, W, H, restrict_view=False, scale=32, food_turns=None, draw_health=False):
+    """render(mode="rgb_array", scale, draw_health) of observations -> u8 [B, W*s, H*s, 3]
+    (draw_health needs food_turns)."""
     planes = np.ascontiguousarray(planes, dtype=np.uint8)
     B, S = planes.shape[0], planes.shape[3]
     out = np.zeros((B, W * scale, H * scale, 3), np.uint8)
     r = np.ascontiguousarray(role, dtype=np.uint8)
     st = np.ascontiguousarray(status, dtype=np.uint8)
-    lib().wabo_render(B, W, H, S, int(bool(restrict_view)), scale, _p(planes), _p(r), _p(st), _p(out))
+    ft = np.ascontiguousarray(np.zeros(B) if food_turns is None else food_turns, dtype=np.uint8)
+    if draw_health and food_turns is None:
+        raise ValueError("draw_health needs food_turns")
+    lib().wabo_render(B, W, H, S, int(bool(restrict_view)), scale, int(bool(draw_health)), _p(planes), _p(ft),
+                      _p(r), _p(st), _p(out))
     return out
 
 

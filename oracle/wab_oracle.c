@@ -10,6 +10,8 @@
  */
 #include "wab_oracle.h"
 
+#include "../wab_gym_amd/csrc/wab_glyphs.h" /* data: PIL digit coverage (tools/make_glyphs.py) */
+
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -502,13 +504,40 @@ void wabo_featurize(int64_t B, int W, int H, int S, int turns_empty, const uint8
   }
 }
 
-/* render (wab_env.py:468-502), draw_health=False: channel c of cell (i, j) is 255 * grid_c;
- * an empty cell is 127 when killed, else 255 and then every channel goes through mask_grid
- * with the ostrich's role (:490-493: blind spots 0, only under restrict_view); each cell
- * becomes a scale x scale block (:494).  The grids are the observation's (already masked,
- * which mask_grid leaves unchanged). */
-void wabo_render(int64_t B, int W, int H, int S, int restrict_view, int scale, const uint8_t* planes,
-                 const uint8_t* role, const uint8_t* status, uint8_t* rgb) {
+static const uint8_t GLYPHS_FLAT[10 * WAB_GLYPH_ROWS * WAB_GLYPH_ADVANCE] = {WAB_GLYPH_DATA};
+
+/* draw_health (:496-500): ImageDraw.text((0, 0), str(food), fill="blue") on the scaled image,
+ * PIL's default font: each digit's coverage a (wab_glyphs.h, baked from PIL by
+ * tools/make_glyphs.py) blends the ink in by Pillow's rule DIV255(x * (255 - a) + ink * a) */
+static void draw_count(uint8_t* img, int RW, int RH, int count) {
+  char txt[8];
+  int nd = 0;
+  for (int v = count;; v /= 10) { txt[nd++] = (char)('0' + v % 10); if (v < 10) break; }
+  for (int k = 0; k < nd; ++k) {
+    const int digit = txt[nd - 1 - k] - '0';
+    for (int r = 0; r < WAB_GLYPH_ROWS; ++r)
+      for (int c = 0; c < WAB_GLYPH_ADVANCE; ++c) {
+        const int y = WAB_GLYPH_ROW0 + r, x = k * WAB_GLYPH_ADVANCE + c;  /* PIL (x, y) = (axis 1, axis 0) */
+        if (y >= RW || x >= RH) continue;
+        const unsigned a = GLYPHS_FLAT[(digit * WAB_GLYPH_ROWS + r) * WAB_GLYPH_ADVANCE + c];
+        uint8_t* px = img + ((size_t)y * RH + (size_t)x) * 3;
+        for (int ch = 0; ch < 3; ++ch) {
+          const unsigned ink = ch == 2 ? WAB_GLYPH_INK_B : 0u;
+          const unsigned t = (unsigned)px[ch] * (255u - a) + ink * a + 128u;
+          px[ch] = (uint8_t)(((t >> 8) + t) >> 8);
+        }
+      }
+  }
+}
+
+/* render (wab_env.py:468-502): channel c of cell (i, j) is 255 * grid_c; an empty cell is 127
+ * when killed, else 255 and then every channel goes through mask_grid with the ostrich's role
+ * (:490-493: blind spots 0, only under restrict_view); each cell becomes a scale x scale block
+ * (:494); draw_health draws the turns-until-starve count (:496-500).  The grids are the
+ * observation's (already masked, which mask_grid leaves unchanged). */
+void wabo_render(int64_t B, int W, int H, int S, int restrict_view, int scale, int draw_health,
+                 const uint8_t* planes, const uint8_t* food_turns, const uint8_t* role, const uint8_t* status,
+                 uint8_t* rgb) {
   const int RW = W * scale, RH = H * scale;
   for (int64_t e = 0; e < B; ++e) {
     const uint8_t* pl = planes + (size_t)e * 3 * W * S;
@@ -528,6 +557,7 @@ void wabo_render(int64_t B, int W, int H, int S, int restrict_view, int scale, c
             px[2] = c[2];
           }
       }
+    if (draw_health) draw_count(img, RW, RH, food_turns[e]);
   }
 }
 

@@ -599,8 +599,9 @@ def test_superbasic_matches_reference_golden_and_oracle():
 
 
 def test_render_matches_reference_frames_and_oracle():
-    """f3: device render == the reference's rgb_array frames (draw_health=False), and == the
-    oracle on live observations (31x31, restrict_view, killed envs)."""
+    """f3: device render == the reference's rgb_array frames, with the draw_health text (its
+    default) at scales 2, 32 and 1 and without it, and == the oracle on live observations
+    (31x31, restrict_view, killed envs)."""
     import torch
 
     from oracle import oracle as orc
@@ -611,13 +612,24 @@ def test_render_matches_reference_frames_and_oracle():
     for si, name in enumerate(names):
         sel = z["set"] == si
         n = int(sel.sum())
-        opts = {"restrict_view": True, "lookout_only": False} if name == "restrict" else None
+        opts = {"restrict": {"restrict_view": True, "lookout_only": False},
+                "longfood": {"turns_to_empty_food": 150}}.get(name)
         env = _env(opts, n)
         env.reset()
         env._obs["planes"].copy_(torch.as_tensor(z["planes"][sel]))
         env._obs["scalars"].copy_(torch.as_tensor(np.ascontiguousarray(z["scalars"][sel].T)))
-        img = env.render(scale=scale)
+        img = env.render(scale=scale, draw_health=False)
         assert np.array_equal(img.cpu().numpy(), z["images"][sel]), name
+        img = env.render(scale=scale)  # draw_health=True, the reference's default
+        assert np.array_equal(img.cpu().numpy(), z["images_health"][sel]), name
+        big = np.nonzero(sel[z["big_idx"]])[0]
+        bi = z["big_idx"][big]
+        obs = {"planes": torch.as_tensor(z["planes"][bi]).cuda(),
+               "scalars": torch.as_tensor(np.ascontiguousarray(z["scalars"][bi].T)).cuda()}
+        env_b = _env(opts, len(bi))
+        for s2, key in ((32, "images_health32"), (1, "images_health1")):
+            img = env_b.render(scale=s2, obs=obs)
+            assert np.array_equal(img.cpu().numpy(), z[key][big]), (name, s2)
     for opts in (None, {"width": 31, "height": 31}, {"restrict_view": True, "lookout_only": False},
                  {"chance_wolf_on_square": 0.05}):
         env = _env(opts, 300, validate_actions=False)
@@ -627,11 +639,12 @@ def test_render_matches_reference_frames_and_oracle():
         for _ in range(15):
             env.step(torch.randint(0, env.n_actions, (300,), device="cuda:0", generator=g))
         for scale in (1, 3):
-            img = env.render(scale=scale).cpu().numpy()
-            sc = env._obs["scalars"].cpu().numpy()
-            want = orc.render(env._obs["planes"].cpu().numpy(), sc[1], sc[2], env.W, env.H,
-                              env.game_options["restrict_view"], scale)
-            assert np.array_equal(img, want)
+            for dh in (False, True):
+                img = env.render(scale=scale, draw_health=dh).cpu().numpy()
+                sc = env._obs["scalars"].cpu().numpy()
+                want = orc.render(env._obs["planes"].cpu().numpy(), sc[1], sc[2], env.W, env.H,
+                                  env.game_options["restrict_view"], scale, food_turns=sc[0], draw_health=dh)
+                assert np.array_equal(img, want)
 
 
 def test_discounted_returns_match_oracle():

@@ -71,7 +71,7 @@ def load():
     L.wab_superbasic_dim.argtypes = [P]
     L.wab_featurize_superbasic.argtypes = [P, P, P, P]
     L.wab_step_features.argtypes = [P, P, P, P, P, P, P]
-    L.wab_render.argtypes = [P, P, I32, P, P]
+    L.wab_render.argtypes = [P, P, I32, I32, P, P]
     L.wab_egocentric.argtypes = [P, P, P, P]
     L.wab_debug_bush_values.argtypes = [P, P, P, I64, P]
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]

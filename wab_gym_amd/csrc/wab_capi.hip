@@ -727,7 +727,7 @@ int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features,
   return featurize(h, 1, obs, nullptr, features, stream, "wab_featurize_superbasic");
 }
 
-int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, void* stream) {
+int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, int32_t draw_health, uint8_t* rgb, void* stream) {
   g_err.clear();
   if (!h || !rgb) return fail(WAB_E_INVALID, "wab_render: NULL argument");
   if (int rc = check_obs(obs, "wab_render")) return rc;
@@ -740,9 +740,11 @@ int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, v
   rp.W = p.W; rp.H = p.H; rp.S = p.S; rp.OB = p.OB;
   rp.scale = scale;
   rp.restrict_view = p.restrict_view;
+  rp.draw_health = draw_health != 0;
   rp.B = p.B;
   std::memcpy(rp.mask_rows, p.mask_rows, sizeof(rp.mask_rows));
   rp.planes = obs->planes;
+  rp.food_turns = obs->food_turns;
   rp.role = obs->role;
   rp.status = obs->status;
   rp.rgb = rgb;
@@ -754,6 +756,7 @@ int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, uint8_t* rgb, v
   for (int64_t e0 = 0; e0 < p.B; e0 += 65535) {  // grid.y is at most 65535 envs per launch
     wab::RenderParams r2 = rp;
     r2.planes = rp.planes + (size_t)e0 * p.OB;
+    r2.food_turns = rp.food_turns + e0;
     r2.role = rp.role + e0;
     r2.status = rp.status + e0;
     r2.rgb = rp.rgb + (size_t)e0 * per_env;

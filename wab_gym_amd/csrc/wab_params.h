@@ -242,9 +242,11 @@ struct FeatParams {
 // wab_render (wab_render.hip)
 struct RenderParams {
   int32_t W, H, S, OB, scale, restrict_view;
+  int32_t draw_health;       // the turns-until-starve text overlay (wab_env.py:496-500)
   int64_t B;
   uint32_t mask_rows[2][11];
   const uint8_t* planes;
+  const uint8_t* food_turns;
   const uint8_t* role;
   const uint8_t* status;
   uint8_t* rgb;

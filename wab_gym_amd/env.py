@@ -236,19 +236,29 @@ class BatchedWolvesAndBushesEnv:
                    "wab_rollout")
         return planes, scal.permute(1, 0, 2), rew, done
 
-    def render(self, mode="rgb_array", scale=32, draw_health=False, out=None):
-        """render (wab_env.py:468-502) of every env's current observation on device:
-        u8 [B, W*scale, H*scale, 3].  Only mode "rgb_array" and draw_health=False (the
-        reference's food-count text uses PIL's default font, not reproduced)."""
+    def render(self, mode="rgb_array", scale=32, draw_health=True, out=None, obs=None):
+        """render (wab_env.py:468-502) of every env's current observation (or of `obs`, a
+        dict of planes [B,3,W,S] and scalars [3,B] u8 tensors) on device: u8 [B, W*scale,
+        H*scale, 3].  draw_health (the reference's default) draws the turns-until-starve
+        count in blue at (0, 0) with PIL's default font's digit glyphs (tools/make_glyphs.py;
+        parity with the reference's pinned Pillow 7.2 font is unpinned)."""
         if mode != "rgb_array":
             raise NotImplementedError("only mode='rgb_array' (wab_env.py:104 metadata)")
-        if draw_health:
-            raise NotImplementedError("draw_health=True (PIL text overlay) is not reproduced")
         t = self._torch
         shape = (self.num_envs, self.W * scale, self.H * scale, 3)
         img = t.empty(shape, dtype=t.uint8, device=self.device) if out is None else out
-        _lib.check(_lib.load().wab_render(self._h, ctypes.addressof(self._obs["struct"]), int(scale),
+        if tuple(img.shape) != shape or img.dtype != t.uint8 or not img.is_contiguous() or img.device != self.device:
+            raise ValueError("out must be a contiguous uint8 tensor of shape %s on %s" % (shape, self.device))
+        keep = None
+        if obs is None:
+            st = self._obs["struct"]
+        else:
+            planes, scal = obs["planes"].contiguous(), obs["scalars"].contiguous()
+            st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr())
+            keep = (planes, scal)
+        _lib.check(_lib.load().wab_render(self._h, ctypes.addressof(st), int(scale), int(bool(draw_health)),
                                           img.data_ptr(), self._stream()), "wab_render")
+        del keep
         return img
 
     @property
