@@ -219,8 +219,8 @@ def main():
                 i = t % T
                 _lib.check(c5_step(t, i, s), "c5 step")
                 if i == T - 1:
-                    _lib.check(L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s),
-                               "wab_discounted_returns")
+                    _lib.check(L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s),
+                               "wab_discounted_returns_exact")
     else:
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
@@ -300,7 +300,7 @@ def main():
             return e0.elapsed_time(e1) / n
 
         n_k = min(K, 512)
-        ret_ms = per_launch(lambda i: L.wab_discounted_returns(r0, d0, T, B, 0.99, None, ret0, s), 64)
+        ret_ms = per_launch(lambda i: L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s), 64)
         if fused:
             sf_ms = per_launch(lambda i: L.wab_step_features(h, a0 + (W + i) * B, fobs_addr, rew, done,
                                                              f0 + 4 * (i % T) * B * F, s), n_k)

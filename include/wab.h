@@ -30,6 +30,7 @@
  *                            _get_bush_proximities                   wab_env.py:652-667
  *                            + gym.spaces.flatten                    actor_critic.py:188
  *   wab_discounted_returns<- finish_episode's return loop             actor_critic.py:139-143
+ *   wab_discounted_returns_exact <- the same on the env's own rewards   actor_critic.py:139-145
  */
 #ifndef WAB_H_
 #define WAB_H_
@@ -241,6 +242,16 @@ int wab_egocentric(wab_handle* h, const uint8_t* mask, uint8_t* proximity, void*
  * written as f32.  All pointers device. */
 int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, int64_t B,
                            double gamma, const float* bootstrap, float* returns, void* stream);
+
+/* wab_discounted_returns over rewards that this handle's steps returned: each float32 reward
+ * is first mapped back to the exact double the reference's step() returns (0 + r_x or
+ * 0 + r_eat + r_x, wab_env.py:251-340; e.g. -0.8999999999999999 for 0.1 + -1, whose float32
+ * is -0.9f), so the returns equal float32 of finish_episode's own double returns
+ * (actor_critic.py:139-145) bit for bit.  Rewards outside that set are used as given.
+ * WAB_E_INVALID if two of the options' rewards round to the same float32. */
+int wab_discounted_returns_exact(const wab_handle* h, const float* reward, const uint8_t* done, int32_t T,
+                                 int64_t B, double gamma, const float* bootstrap, float* returns,
+                                 void* stream);
 
 /* Test hook: the bush value (berries, generate_n_bush_values wab_env.py:631-635) the step
  * kernels give the 53-bit draws U[n] under h's threshold table, computed by the kernels' own

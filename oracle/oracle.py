@@ -55,7 +55,8 @@ def lib():
         L.wabo_superbasic_dim.argtypes = [ctypes.c_int] * 3
         L.wabo_render.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 6 + [P] * 5
         L.wabo_featurize_superbasic.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 5
-        L.wabo_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_double, P, P]
+        L.wabo_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_double, P, P, P,
+                                              ctypes.c_int]
         _lib = L
     return _lib
 
@@ -182,11 +183,14 @@ def render(planes, role, status, W, H, restrict_view=False, scale=32, food_turns
     return out
 
 
-def discounted_returns(reward, done, gamma=0.99, bootstrap=None):
+def discounted_returns(reward, done, gamma=0.99, bootstrap=None, exact_values=None):
+    """exact_values: the doubles one step can return (their float32 stands for them)."""
     reward = np.ascontiguousarray(reward, dtype=np.float32)
     done = np.ascontiguousarray(done, dtype=np.uint8)
     T, B = reward.shape
     out = np.zeros((T, B), np.float32)
     bs = None if bootstrap is None else np.ascontiguousarray(bootstrap, dtype=np.float32)
-    lib().wabo_discounted_returns(T, B, _p(reward), _p(done), gamma, _p(bs), _p(out))
+    ev = None if exact_values is None else np.ascontiguousarray(exact_values, dtype=np.float64)
+    lib().wabo_discounted_returns(T, B, _p(reward), _p(done), gamma, _p(bs), _p(out), _p(ev),
+                                  0 if ev is None else len(ev))
     return out

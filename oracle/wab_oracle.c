@@ -617,14 +617,21 @@ void wabo_featurize_superbasic(int64_t B, int W, int H, int S, int turns_empty, 
 }
 
 /* actor_critic.finish_episode returns (actor_critic.py:139-143): per env, reverse
- * R = r + gamma * R in double (Python floats), restarting after each done; f32 out */
+ * R = r + gamma * R in double (Python floats), restarting after each done; f32 out.  The
+ * rewards are the float32 device rewards; a reward whose float32 equals that of one of the
+ * exact_values (the doubles a step can return) stands for that double. */
 void wabo_discounted_returns(int64_t T, int64_t B, const float* reward, const uint8_t* done,
-                             double gamma, const float* bootstrap, float* out) {
+                             double gamma, const float* bootstrap, float* out, const double* exact_values,
+                             int n_exact) {
   for (int64_t b = 0; b < B; ++b) {
     double R = bootstrap ? (double)bootstrap[b] : 0.0;
     for (int64_t t = T - 1; t >= 0; --t) {
       if (done[t * B + b]) R = 0.0;
-      R = (double)reward[t * B + b] + gamma * R;
+      const float rf = reward[t * B + b];
+      double r = (double)rf;
+      for (int k = 0; k < n_exact; ++k)
+        if ((float)exact_values[k] == rf) r = exact_values[k];
+      R = r + gamma * R;
       out[t * B + b] = (float)R;
     }
   }

@@ -17,7 +17,7 @@ EXPORTED = [
     "wab_reset", "wab_step", "wab_rollout", "wab_get_counters", "wab_get_state", "wab_batch",
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
-    "wab_debug_bush_values", "wab_step_features",
+    "wab_debug_bush_values", "wab_step_features", "wab_discounted_returns_exact",
 ]
 
 ABI_VERSION = 2
@@ -75,6 +75,7 @@ def load():
     L.wab_egocentric.argtypes = [P, P, P, P]
     L.wab_debug_bush_values.argtypes = [P, P, P, I64, P]
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
+    L.wab_discounted_returns_exact.argtypes = [P, P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64
     L.wab_step_kernel.argtypes = [P]

@@ -31,7 +31,7 @@ __global__ void wab_featurize_small_kernel(FeatParams p);
 __global__ void wab_render_kernel(RenderParams p);
 __global__ void wab_egocentric_kernel(EgoParams p);
 __global__ void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T, int64_t B,
-                                   double gamma, const float* bootstrap, float* out);
+                                   double gamma, const float* bootstrap, float* out, RewardTable tab);
 }
 
 using wab::Params;
@@ -53,6 +53,7 @@ struct wab_handle {
   uint32_t* ego_diamond = nullptr;
   int ego_cap = 0, ego_n_diamond = 0;
   bool small_g11 = false;    // the small kernel's 11x11 specialisation (geometry_11)
+  wab::RewardTable rewards;  // exact doubles of the rewards a step returns (n = 0: ambiguous)
   size_t wide_lds_bytes = 0;  // LDS per workgroup of the wide kernel (see wab_create)
 };
 
@@ -332,6 +333,27 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   p.r_starve = c->reward_for_starving;
   p.r_finish = c->reward_for_finishing;
   p.r_eat = c->reward_for_eating;
+  {  // the step's possible rewards, accumulated from 0 as wab_env.py:251-340 does
+    wab::RewardTable& t = h->rewards;
+    t.n = 0;
+    const double rx[4] = {p.r_turn, p.r_finish, p.r_starve, p.r_killed};
+    bool ok = true;
+    for (int k = 0; k < 4 && ok; ++k)
+      for (int eat = 0; eat < 2 && ok; ++eat) {
+        const double d = eat ? (0.0 + p.r_eat) + rx[k] : 0.0 + rx[k];
+        const float f = (float)d;
+        uint32_t fb;
+        std::memcpy(&fb, &f, 4);
+        bool dup = false;
+        for (int i = 0; i < t.n; ++i)
+          if (t.f32[i] == fb) {
+            dup = true;
+            if (t.f64[i] != d) ok = false;  // two doubles, one float32: not recoverable
+          }
+        if (!dup) { t.f32[t.n] = fb; t.f64[t.n] = d; t.n++; }
+      }
+    if (!ok) t.n = -1;
+  }
   p.start_food = c->starting_food;
   p.start_role = c->starting_role;
   p.start_food_random = c->starting_food_random;
@@ -821,8 +843,26 @@ int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, 
   if (!reward || !done || !returns || T < 0 || B < 0)
     return fail(WAB_E_INVALID, "wab_discounted_returns: bad argument");
   if (T == 0 || B == 0) return WAB_OK;
+  wab::RewardTable none;
+  std::memset(&none, 0, sizeof(none));
   hipLaunchKernelGGL(wab::wab_returns_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns);
+                     (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns, none);
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+
+int wab_discounted_returns_exact(const wab_handle* h, const float* reward, const uint8_t* done, int32_t T,
+                                 int64_t B, double gamma, const float* bootstrap, float* returns, void* stream) {
+  g_err.clear();
+  if (!h || !reward || !done || !returns || T < 0 || B < 0)
+    return fail(WAB_E_INVALID, "wab_discounted_returns_exact: bad argument");
+  if (h->rewards.n < 0)
+    return fail(WAB_E_INVALID, "wab_discounted_returns_exact: two of the options' rewards round to the same "
+                               "float32; the double rewards are not recoverable");
+  if (T == 0 || B == 0) return WAB_OK;
+  DeviceGuard guard(h->device);
+  hipLaunchKernelGGL(wab::wab_returns_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns, h->rewards);
   HIP_TRY(hipGetLastError());
   return WAB_OK;
 }

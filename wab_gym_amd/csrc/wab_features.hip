@@ -297,14 +297,20 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
 // actor_critic.finish_episode returns (actor_critic.py:139-143), one thread per env
 __global__ __launch_bounds__(256) void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T,
                                                           int64_t B, double gamma, const float* bootstrap,
-                                                          float* out) {
+                                                          float* out, RewardTable tab) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   double R = bootstrap ? (double)bootstrap[b] : 0.0;
   for (int32_t t = T - 1; t >= 0; --t) {
     const int64_t i = (int64_t)t * B + b;
     if (done[i]) R = 0.0;
-    R = (double)reward[i] + gamma * R;
+    // the step's exact double reward when the table has it (the env's own rewards), else the
+    // float32 as given
+    const float rf = reward[i];
+    double r = (double)rf;
+    for (int k = 0; k < tab.n; ++k)
+      if (__float_as_uint(rf) == tab.f32[k]) r = tab.f64[k];
+    R = r + gamma * R;  // (no contraction: -ffp-contract=off, the reference's op order)
     out[i] = (float)R;
   }
 }

@@ -239,6 +239,15 @@ struct FeatParams {
   float* out;                // [B][F]
 };
 
+// The rewards one step of an env can return (wab_env.py:299-340: 0 + r_x, or 0 + r_eat + r_x
+// for r_x in per turn / finishing / starving / killed) as (float32 bits, exact double) pairs:
+// the double a float32 device reward came from (wab_discounted_returns_exact).  n = 0: none.
+struct RewardTable {
+  int32_t n;
+  uint32_t f32[8];
+  double f64[8];
+};
+
 // wab_render (wab_render.hip)
 struct RenderParams {
   int32_t W, H, S, OB, scale, restrict_view;

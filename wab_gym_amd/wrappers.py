@@ -125,20 +125,31 @@ class SuperBasicObservationWrapper(PragmaticObsWrapper):
         return dst
 
 
-def discounted_returns(reward, done, gamma=0.99, bootstrap=None, out=None):
+def discounted_returns(reward, done, gamma=0.99, bootstrap=None, out=None, env=None):
     """R_t = r_t + gamma * R_{t+1}, restarted after each done (actor_critic.py:139-143),
-    over [T, B] device tensors; one HIP kernel, double accumulation, float32 out."""
+    over [T, B] device tensors; one HIP kernel, double accumulation, float32 out.  With `env`
+    (the env whose steps returned `reward`) each float32 reward is first mapped back to the
+    exact double the reference's step() returns, so the result is float32 of finish_episode's
+    own double returns bit for bit (wab_discounted_returns_exact)."""
     import torch
 
     r = reward.to(torch.float32).contiguous()
     d = done.to(torch.uint8).contiguous()
     T, B = r.shape
+    if d.shape != (T, B):
+        raise ValueError("done must have the shape of reward [T, B]")
     o = torch.empty_like(r) if out is None else out
+    if o.shape != (T, B) or o.dtype != torch.float32 or not o.is_contiguous():
+        raise ValueError("out must be a contiguous float32 tensor of shape [T, B]")
     bs = None if bootstrap is None else bootstrap.to(torch.float32).contiguous()
     stream = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
-    _lib.check(_lib.load().wab_discounted_returns(r.data_ptr(), d.data_ptr(), T, B, float(gamma),
-                                                  None if bs is None else bs.data_ptr(), o.data_ptr(),
-                                                  stream), "wab_discounted_returns")
+    L = _lib.load()
+    args = (r.data_ptr(), d.data_ptr(), T, B, float(gamma), None if bs is None else bs.data_ptr(), o.data_ptr(),
+            stream)
+    if env is None:
+        _lib.check(L.wab_discounted_returns(*args), "wab_discounted_returns")
+    else:
+        _lib.check(L.wab_discounted_returns_exact(env._h, *args), "wab_discounted_returns_exact")
     return o
 
 
