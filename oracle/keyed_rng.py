@@ -21,6 +21,20 @@ Call sites in the reference and the key they get (site ids):
                                              among the wolves in list order
   4  starting food     `spawn_ostriches` (`:597`, only if starting_food is None)  tile (0, 0)
   5  starting role     `spawn_ostriches` (`:599`, randint(2))                    tile (0, 0)
+  6  spawn gaps        the wolf-spawn draws of sites 2 (below), turn, "tile" (k, 0) = k-th gap
+
+Wolf spawns (site 2) are drawn as a *set*, not tile by tile.  The reference draws one
+uniform per candidate tile and spawns a wolf where u < q (`:573`, `:590`): iid
+Bernoulli(q) over the tiles.  The same joint law is drawn here by geometric gaps over a
+canonical tile order (the ring order `ring_index`, or the view-cell order `view_index`
+for `initialize_wolves`): the number of misses before the next hit among the m tiles left
+is G = #{g in 1..m : U_k < P[g]}, P[g] = floor((1 - q)^g * 2^53) (`gap_thresholds`), with
+U_k the site-6 draw of the k-th gap; G = m ends the set (`spawn_hits`).  A step with no
+spawn (~97.6 % at the defaults) costs ONE draw instead of one per ring tile.  The
+per-tile uniforms the reference sees are then drawn conditionally on the set
+(`conditional_spawn_U`: below q on a hit tile, at or above q elsewhere, each from the
+tile's own site-2 draw), so the reference's comparison returns exactly the set and the
+vector it receives is still iid U(0, 1) (to the 2^-53 grid).
 
 Definition (all arithmetic mod 2^64 / 2^32):
     mix64(z)    = splitmix64 finaliser
@@ -48,6 +62,7 @@ SITE_SPAWN = 2
 SITE_DESPAWN = 3
 SITE_START_FOOD = 4
 SITE_START_ROLE = 5
+SITE_GAP = 6
 
 
 def mix64(z: int) -> int:
@@ -118,3 +133,72 @@ def hit_threshold_lt(p: float) -> int:
 def bush_value_from_u(u, power, max_berries):
     """The reference's arithmetic, `wab_env.py:632-635`, evaluated by numpy on arrays."""
     return np.round(np.asarray(u, dtype=np.float64) ** power * max_berries)
+
+
+# ----------------------------------------------------------------------------------------
+# wolf spawns as a set: geometric gaps (site 6) over a canonical tile order
+# ----------------------------------------------------------------------------------------
+def gap_thresholds(T: int, n: int) -> list:
+    """P[g], g = 0..n: floor((1 - q)^g * 2^53), q = T * 2^-53 (T = hit_threshold_lt(p)).
+
+    The power is a running product in IEEE double (1 - q is exact), the scaling by 2^53
+    exact, so C (wab_capi.hip, wab_oracle.c) and Python get the same integers."""
+    omq = float(TWO53 - T) * 2.0 ** -53
+    out = [TWO53]
+    p = 1.0
+    for _ in range(n):
+        p = p * omq
+        out.append(int(np.floor(p * float(TWO53))))
+    return out
+
+
+def gap_count(U: int, P: list, m: int) -> int:
+    """Misses before the next hit among m tiles: #{g in 1..m : U < P[g]} (m: no hit)."""
+    lo, hi = 0, m  # P[0] = 2^53 > U; P is non-increasing
+    while lo < hi:
+        mid = (lo + hi + 1) >> 1
+        if U < P[mid]:
+            lo = mid
+        else:
+            hi = mid - 1
+    return lo
+
+
+def spawn_hits(ek: int, turn: int, n: int, P: list) -> list:
+    """Ascending indices in [0, n) of the tiles that spawn a wolf at `turn` (iid Bernoulli(q))."""
+    hits, pos, k = [], 0, 0
+    while pos < n:
+        U = int(draw_U(ek, SITE_GAP, turn, [k & 0xFFFF], [k >> 16], 0)[0])
+        G = gap_count(U, P, n - pos)
+        if G >= n - pos:
+            break
+        pos += G
+        hits.append(pos)
+        pos += 1
+        k += 1
+    return hits
+
+
+def ring_index(dx: int, dy: int, W: int, H: int, margin: int) -> int:
+    """Index of the spawn-ring tile at offset (dx, dy) from the ostrich: the bands of rows
+    below and above the view first (`margin` rows each, x fastest), then the columns left
+    and right of it (y fastest); the order of the kernels' ring table (wab_capi.hip)."""
+    m, Wm = margin, W + 2 * margin
+    xi, yi = dx + W // 2 + m, dy + H // 2 + m
+    if yi < m:
+        return yi * Wm + xi
+    if yi >= m + H:
+        return (yi - H) * Wm + xi
+    band = xi if xi < m else xi - W
+    return 2 * m * Wm + band * H + (yi - m)
+
+
+def view_index(dx: int, dy: int, W: int, H: int) -> int:
+    """Obs cell i * H + j of the tile at offset (dx, dy) = (W//2 - i, H//2 - j)."""
+    return (W // 2 - dx) * H + (H // 2 - dy)
+
+
+def conditional_spawn_U(V: int, T: int, hit: bool) -> int:
+    """A tile's 53-bit uniform given the set: from its own site-2 draw V, below T on a hit
+    tile, at or above T elsewhere (uniform on either side to the 2^-53 grid)."""
+    return (V * T) >> 53 if hit else T + ((V * (TWO53 - T)) >> 53)

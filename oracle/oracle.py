@@ -49,6 +49,9 @@ def lib():
         L.wabo_draw_U.restype = ctypes.c_uint64
         L.wabo_draw_U.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_uint32]
+        L.wabo_spawn_hits.argtypes = [P, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, P, ctypes.c_int]
+        L.wabo_gap_threshold.restype = ctypes.c_uint64
+        L.wabo_gap_threshold.argtypes = [P, ctypes.c_int]
         L.wabo_feature_dim.argtypes = [ctypes.c_int] * 3
         L.wabo_featurize.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 4 + [P] * 6
         L.wabo_egocentric.argtypes = [P, P]
@@ -116,6 +119,15 @@ class OracleBatch:
         out = np.zeros((self.B, 5), np.uint8)
         lib().wabo_egocentric(self.h, _p(out))
         return out
+
+    def spawn_hits(self, ek, turn, n):
+        """The keyed spawn set of n tiles at `turn` (keyed_rng.spawn_hits) under this batch's q."""
+        out = np.zeros(max(n, 1), np.int32)
+        k = lib().wabo_spawn_hits(self.h, ek, turn, n, _p(out), n)
+        return out[:k].tolist()
+
+    def gap_threshold(self, g):
+        return int(lib().wabo_gap_threshold(self.h, g))
 
     def state(self):
         food = np.zeros(self.B, np.float64)

@@ -49,7 +49,44 @@ uint64_t wabo_draw_U(uint64_t ek, uint32_t site, int64_t turn, int64_t x, int64_
   return ((uint64_t)hi << 21) | (uint64_t)(lo >> 11);
 }
 
-enum { SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5 };
+enum { SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5, SITE_GAP = 6 };
+
+/* wolf spawns as a set (keyed_rng.py: gap_thresholds, gap_count, spawn_hits): P[g] =
+ * floor((1 - q)^g 2^53), q = T 2^-53, the power a running product in double */
+static uint64_t* gap_thresholds(uint64_t T, int n) {
+  uint64_t* P = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n + 1));
+  const double omq = ldexp((double)((1ULL << 53) - T), -53);
+  double p = 1.0;
+  P[0] = 1ULL << 53;
+  for (int g = 1; g <= n; ++g) {
+    p = p * omq;
+    P[g] = (uint64_t)floor(ldexp(p, 53));
+  }
+  return P;
+}
+
+/* misses before the next hit among m tiles: #{g in 1..m : U < P[g]} (m: none) */
+static int gap_count(uint64_t U, const uint64_t* P, int m) {
+  int lo = 0, hi = m;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (U < P[mid]) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+/* calls hit(ctx, index) for each tile in [0, n) that spawns a wolf at `turn`, ascending */
+static void spawn_hits(uint64_t ek, int64_t turn, int n, const uint64_t* P, void (*hit)(void*, int), void* ctx) {
+  int pos = 0;
+  for (uint32_t k = 0; pos < n; ++k) {
+    const uint64_t U = wabo_draw_U(ek, SITE_GAP, turn, (int64_t)(k & 0xFFFFu), (int64_t)(k >> 16), 0);
+    const int G = gap_count(U, P, n - pos);
+    if (G >= n - pos) break;
+    pos += G;
+    hit(ctx, pos);
+    pos += 1;
+  }
+}
 
 /* ------------------------------------------------------------------ state */
 typedef struct { int32_t x, y; } xy_t;
@@ -80,6 +117,7 @@ struct wabo_batch {
   int n_actions;
   int act_dx[6], act_dy[6], act_role[6]; /* act_role -1 = NaN (no role change) */
   uint64_t keep_gt, spawn_lt;
+  uint64_t* gap; /* gap_thresholds(spawn_lt, max(ring, view)) */
   double fill, hunger;
   int stride, plane_bytes, obs_bytes;
   oenv* envs;
@@ -182,6 +220,31 @@ static void push_wolf(oenv* e, int32_t x, int32_t y) {
   e->nw++;
 }
 
+/* spawn_hits callbacks: tile index -> wolf (view cell c = i*H + j at (cw - i, ch - j); ring
+ * tile r in the order of keyed_rng.ring_index) */
+typedef struct { oenv* e; int W, H, m; } hit_ctx;
+
+static void push_view_cell(void* v, int c) {
+  const hit_ctx* h = (const hit_ctx*)v;
+  push_wolf(h->e, h->e->x + h->W / 2 - c / h->H, h->e->y + h->H / 2 - c % h->H);
+}
+
+static void push_ring_tile(void* v, int r) {
+  const hit_ctx* h = (const hit_ctx*)v;
+  const int m = h->m, Wm = h->W + 2 * m;
+  int xi, yi;
+  if (r < 2 * m * Wm) {
+    const int band = r / Wm;
+    xi = r % Wm;
+    yi = band < m ? band : band + h->H;
+  } else {
+    const int r2 = r - 2 * m * Wm, band = r2 / h->H;
+    yi = m + r2 % h->H;
+    xi = band < m ? band : band + h->W;
+  }
+  push_wolf(h->e, h->e->x + xi - h->W / 2 - m, h->e->y + yi - h->H / 2 - m);
+}
+
 /* ------------------------------------------------------------------ construction */
 wabo_batch* wabo_create(const wab_config* cfg, int64_t batch, uint64_t seed, int64_t env_id_base) {
   if (cfg->width % 2 == 0 || cfg->height % 2 == 0) return NULL; /* wab_env.py:147-148 */
@@ -202,6 +265,11 @@ wabo_batch* wabo_create(const wab_config* cfg, int64_t batch, uint64_t seed, int
   /* u > despawn keeps a wolf (:263); u < chance/2 spawns one (:573) */
   b->keep_gt = (uint64_t)floor(ldexp(cfg->wolf_chance_to_despawn, 53));
   b->spawn_lt = (uint64_t)ceil(ldexp(cfg->chance_wolf_on_square / 2.0, 53));
+  {
+    const int m = cfg->wolf_spawn_margin, WH = cfg->width * cfg->height;
+    const int R = (cfg->width + 2 * m) * (cfg->height + 2 * m) - WH;
+    b->gap = gap_thresholds(b->spawn_lt, R > WH ? R : WH);
+  }
   b->fill = 1.0 / (double)cfg->turns_to_fill_food;    /* :307-309 */
   b->hunger = 1.0 / (double)cfg->turns_to_empty_food; /* :316 */
   b->stride = cfg->plane_stride > 0 ? cfg->plane_stride : cfg->height;
@@ -225,10 +293,26 @@ void wabo_destroy(wabo_batch* b) {
   }
   free(b->envs);
   free(b->thresholds);
+  free(b->gap);
   free(b);
 }
 
 int wabo_num_actions(const wabo_batch* b) { return b->n_actions; }
+
+typedef struct { int32_t* out; int cap, n; } hits_out;
+static void collect_hit(void* v, int i) {
+  hits_out* h = (hits_out*)v;
+  if (h->n < h->cap) h->out[h->n] = i;
+  h->n++;
+}
+
+int wabo_spawn_hits(const wabo_batch* b, uint64_t ek, int64_t turn, int n, int32_t* out, int cap) {
+  hits_out h = {out, cap, 0};
+  spawn_hits(ek, turn, n, b->gap, collect_hit, &h);
+  return h.n;
+}
+
+uint64_t wabo_gap_threshold(const wabo_batch* b, int g) { return b->gap[g]; }
 
 /* ------------------------------------------------------------------ observation */
 /* grids from the snapshot (wab_env.py:393-444): planes are [3][W][stride] */
@@ -290,11 +374,9 @@ static void reset_one(wabo_batch* b, oenv* e, uint8_t* planes, uint8_t* food_tur
   /* generate_bushes :613-629: values are a tile function; only the seen set is kept */
   seen_clear(e);
   seen_view(b, e);
-  if (c->wolves) { /* initialize_wolves :578-593: every visible tile, turn 0 */
-    const int cw = c->width / 2, ch = c->height / 2;
-    for (int tx = -cw; tx <= cw; ++tx)
-      for (int ty = -ch; ty <= ch; ++ty)
-        if (wabo_draw_U(e->ek, SITE_SPAWN, 0, tx, ty, 0) < b->spawn_lt) push_wolf(e, tx, ty);
+  if (c->wolves) { /* initialize_wolves :578-593: the visible tiles' spawn set, turn 0 */
+    hit_ctx hc = {e, c->width, c->height, 0};
+    spawn_hits(e->ek, 0, c->width * c->height, b->gap, push_view_cell, &hc);
   }
   int center = bush_remaining(b, e, 0, 0);
   render_planes(b, e, center, planes);
@@ -369,12 +451,10 @@ static void step_one(wabo_batch* b, oenv* e, int a, uint8_t* planes, uint8_t* fo
   if (e->food <= 0.0) { e->status = 1; e->food = 0.0; }   /* :319-322 */
   /* :325-326 spawn_wolves (:527-576): ring around the new position */
   if (c->wolves) {
-    const int cw = c->width / 2, ch = c->height / 2, m = c->wolf_spawn_margin;
-    for (int tx = e->x - cw - m; tx <= e->x + cw + m; ++tx)
-      for (int ty = e->y - ch - m; ty <= e->y + ch + m; ++ty) {
-        if (tx >= e->x - cw && tx <= e->x + cw && ty >= e->y - ch && ty <= e->y + ch) continue;
-        if (wabo_draw_U(e->ek, SITE_SPAWN, e->turn, tx, ty, 0) < b->spawn_lt) push_wolf(e, tx, ty);
-      }
+    const int m = c->wolf_spawn_margin;
+    const int R = (c->width + 2 * m) * (c->height + 2 * m) - c->width * c->height;
+    hit_ctx hc = {e, c->width, c->height, m};
+    spawn_hits(e->ek, e->turn, R, b->gap, push_ring_tile, &hc);
   }
   /* :328-340 reward / done */
   int done;

@@ -97,9 +97,7 @@ class _KeyedRandom:
             xs, ys = _ints(nb["x"]), _ints(nb["y"])
             u = kr.draw_u(ek, kr.SITE_BUSH, 0, xs, ys, 0)
         elif fn in ("initialize_wolves", "spawn_wolves"):
-            nw = frame.f_locals["new_wolves"]
-            xs, ys = _ints(nw["x"]), _ints(nw["y"])
-            u = kr.draw_u(ek, kr.SITE_SPAWN, int(env.current_turn), xs, ys, 0)
+            u = _spawn_draws(env, ek, fn, frame.f_locals["new_wolves"])
         elif fn == "step":
             w = env.wolves
             xs, ys = _ints(w["x"]), _ints(w["y"])
@@ -132,6 +130,31 @@ class _KeyedRandom:
 
 def _ints(series):
     return np.rint(np.asarray(series, dtype=np.float64)).astype(np.int64)
+
+
+def _spawn_draws(env, ek, fn, new_wolves):
+    """The per-tile uniforms of initialize_wolves / spawn_wolves (`wab_env.py:578-593`,
+    `:527-576`), drawn conditionally on the keyed spawn set (keyed_rng.spawn_hits): the set
+    over the view cells at turn 0, or over the ring around the ostrich at the current turn."""
+    o = env.game_options
+    W, H = int(o["width"]), int(o["height"])
+    turn = int(env.current_turn)
+    T = kr.hit_threshold_lt(o["chance_wolf_on_square"] / 2)
+    ox, oy = (int(round(float(v))) for v in (env.ostriches.iloc[0].x, env.ostriches.iloc[0].y))
+    xs, ys = _ints(new_wolves["x"]), _ints(new_wolves["y"])
+    if fn == "initialize_wolves":
+        idx = [kr.view_index(x - ox, y - oy, W, H) for x, y in zip(xs.tolist(), ys.tolist())]
+        n = W * H
+    else:
+        m = int(o["wolf_spawn_margin"])
+        idx = [kr.ring_index(x - ox, y - oy, W, H, m) for x, y in zip(xs.tolist(), ys.tolist())]
+        n = (W + 2 * m) * (H + 2 * m) - W * H
+    if sorted(idx) != list(range(n)):
+        raise RuntimeError("keyed RNG: %s tiles are not the %d-tile canonical set" % (fn, n))
+    hits = set(kr.spawn_hits(ek, turn, n, kr.gap_thresholds(T, n)))
+    V = kr.draw_U(ek, kr.SITE_SPAWN, turn, xs, ys, 0)
+    U = [kr.conditional_spawn_U(int(v), T, i in hits) for v, i in zip(V.tolist(), idx)]
+    return np.asarray(U, dtype=np.float64) * 2.0 ** -53
 
 
 np_proxy = types.SimpleNamespace(**{k: getattr(np, k) for k in dir(np) if not k.startswith("__")})

@@ -46,3 +46,79 @@ def test_integer_thresholds_equal_float_compares():
         u = U.astype(np.float64) * 2.0**-53
         assert np.array_equal(U > keep, u > p)
         assert np.array_equal(U < hit, u < p)
+
+
+def _batch(chance, **kw):
+    opts = {"chance_wolf_on_square": chance}
+    opts.update(kw)
+    return orc.OracleBatch(opts, batch=1)
+
+
+def test_gap_thresholds_match_c():
+    for chance, margin in ((0.001, 1), (0.02, 1), (0.06, 2), (0.0, 1), (1.0, 1)):
+        b = _batch(chance, wolf_spawn_margin=margin)
+        T = kr.hit_threshold_lt(chance / 2)
+        n = max((11 + 2 * margin) ** 2 - 121, 121)
+        P = kr.gap_thresholds(T, n)
+        assert P[0] == 2**53 and all(P[g] >= P[g + 1] for g in range(n))
+        for g in range(n + 1):
+            assert P[g] == b.gap_threshold(g), (chance, g)
+
+
+def test_spawn_hits_match_c():
+    b = _batch(0.06)
+    T = kr.hit_threshold_lt(0.03)
+    P = kr.gap_thresholds(T, 121)
+    for ep in range(40):
+        ek = kr.episode_key(0x5EED, 77, ep)
+        for turn in range(0, 60, 7):
+            for n in (48, 121, 5, 0):
+                assert kr.spawn_hits(ek, turn, n, P) == b.spawn_hits(ek, turn, n)
+
+
+def test_spawn_sets_are_iid_bernoulli():
+    """The gap construction gives every tile probability q, independently: the per-index hit
+    rate is flat and the set size is Binomial(n, q)."""
+    q_chance = 0.2  # q = 0.1: enough hits for a tight check
+    T = kr.hit_threshold_lt(q_chance / 2)
+    q = T / 2**53
+    n = 48
+    P = kr.gap_thresholds(T, n)
+    counts = np.zeros(n)
+    sizes = []
+    N = 6000
+    for env in range(N):
+        h = kr.spawn_hits(kr.episode_key(1, env, 0), 5, n, P)
+        counts[h] += 1
+        sizes.append(len(h))
+    sd = np.sqrt(q * (1 - q) / N)
+    assert np.all(np.abs(counts / N - q) < 5 * sd)
+    sizes = np.asarray(sizes)
+    assert abs(sizes.mean() - n * q) < 5 * np.sqrt(n * q * (1 - q) / N)
+    assert abs(sizes.var() - n * q * (1 - q)) < 0.15 * n * q * (1 - q)
+    # pairwise independence of two fixed tiles
+    both = 0
+    for env in range(N):
+        h = set(kr.spawn_hits(kr.episode_key(1, env, 0), 5, n, P))
+        both += (3 in h) and (40 in h)
+    assert abs(both / N - q * q) < 5 * np.sqrt(q * q / N)
+
+
+def test_conditional_spawn_U_sides():
+    T = kr.hit_threshold_lt(0.0005)
+    rng = np.random.RandomState(3)
+    for V in list(rng.randint(0, 2**53, size=200, dtype=np.int64)) + [0, 2**53 - 1]:
+        lo = kr.conditional_spawn_U(int(V), T, True)
+        hi = kr.conditional_spawn_U(int(V), T, False)
+        assert 0 <= lo < T <= hi < 2**53
+        assert (lo * 2.0**-53 < 0.0005) and not (hi * 2.0**-53 < 0.0005)
+
+
+def test_ring_and_view_index_are_bijections():
+    for W, H, m in ((11, 11, 1), (13, 11, 2), (31, 31, 1), (3, 5, 3)):
+        cw, ch = W // 2, H // 2
+        ring = [kr.ring_index(dx, dy, W, H, m) for dx in range(-cw - m, cw + m + 1)
+                for dy in range(-ch - m, ch + m + 1) if abs(dx) > cw or abs(dy) > ch]
+        assert sorted(ring) == list(range((W + 2 * m) * (H + 2 * m) - W * H))
+        view = [kr.view_index(dx, dy, W, H) for dx in range(-cw, cw + 1) for dy in range(-ch, ch + 1)]
+        assert sorted(view) == list(range(W * H))

@@ -132,8 +132,11 @@ bool small_map(const Params& p) { return p.WHW <= 4; }
 // row).  WAB_STEP_KERNEL=block selects the block kernel for all (A/B measurements).
 enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1, KERNEL_WIDE = 2 };
 
+// (W, H >= 3: the strip that scrolls into view, drawn on another wave, never holds the
+// ostrich's tile)
 bool small_view(const Params& p) {
-  return p.WH <= 128 && p.S == p.H && p.R <= 128 && (!p.restrict_view || (p.W == 11 && p.H == 11));
+  return p.WH <= 128 && p.W >= 3 && p.H >= 3 && p.S == p.H && p.R <= 128 &&
+         (!p.restrict_view || (p.W == 11 && p.H == 11));
 }
 
 // the default options' geometry (11x11 in 11-byte rows, a 48-tile spawn ring): the small
@@ -324,8 +327,23 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   p.bush_power = (float)c->bush_power;
   const uint64_t bush_ge = p.max_berries > 0 ? c->bush_thresholds[0] : (1ull << 53);          // food > 0
   split_threshold(keep_ge, &p.keep_th, &p.keep_tl);
-  split_threshold(spawn_ge, &p.spawn_th, &p.spawn_tl);
   split_threshold(bush_ge, &p.bush_th, &p.bush_tl);
+  // keyed spawn sets (oracle/keyed_rng.py gap_thresholds): gap[g] = floor((1 - q)^g 2^53),
+  // the power a running product in double (1 - q exact), so the oracle gets the same table
+  p.n_gap = p.R > p.WH ? p.R : p.WH;
+  std::vector<uint64_t> gap_host((size_t)p.n_gap + 1);
+  {
+    const double omq = std::ldexp((double)((1ull << 53) - spawn_ge), -53);
+    double q = 1.0;
+    gap_host[0] = 1ull << 53;
+    for (int g = 1; g <= p.n_gap; ++g) {
+      q = q * omq;
+      gap_host[(size_t)g] = (uint64_t)std::floor(std::ldexp(q, 53));
+    }
+    p.gap_inv_l2 = spawn_ge > 0 ? (float)(1.0 / std::log2(omq)) : 0.0f;
+    split_threshold(gap_host[(size_t)p.R], &p.gap_ring_th, &p.gap_ring_tl);
+    split_threshold(gap_host[(size_t)p.WH], &p.gap_view_th, &p.gap_view_tl);
+  }
   p.fill = 1.0 / (double)c->turns_to_fill_food;
   p.hunger = 1.0 / (double)c->turns_to_empty_food;
   p.r_turn = c->reward_per_turn;
@@ -429,6 +447,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   rc |= alloc((void**)&p.block_resets, (size_t)(h->n_blocks > 0 ? h->n_blocks : 1) * 8);
   uint64_t* thr = nullptr;
   rc |= alloc((void**)&thr, (size_t)(p.max_berries > 0 ? p.max_berries : 1) * 8);
+  uint64_t* gap = nullptr;
+  rc |= alloc((void**)&gap, gap_host.size() * 8);
   uint32_t* tab = nullptr;
   p.ring_at = (p.WH + 3) & ~3;
   const int n_tab = p.ring_at + ((p.R + 3) & ~3) + 4;  // + the kernel's one-ahead prefetch
@@ -439,6 +459,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     return fail(WAB_E_NOMEM, msg);
   }
   p.thresholds = thr;
+  p.gap = gap;
   p.tables = tab;
   hipError_t e = hipSuccess;
   {  // view-cell offsets (cw - i, ch - j) for cell i*H + j, then the spawn-ring offsets
@@ -460,6 +481,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     }
     e = hipMemcpy(tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
   }
+  if (e == hipSuccess) e = hipMemcpy(gap, gap_host.data(), gap_host.size() * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess && p.max_berries > 0)
     e = hipMemcpy(thr, c->bush_thresholds, (size_t)p.max_berries * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess && B > 0) {  // every env: episode 0xFFFFFFFF (the first reset makes it 0)

@@ -8,7 +8,9 @@
 
 namespace wab {
 
-enum : uint32_t { SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5 };
+enum : uint32_t {
+  SITE_BUSH = 1, SITE_SPAWN = 2, SITE_DESPAWN = 3, SITE_START_FOOD = 4, SITE_START_ROLE = 5, SITE_GAP = 6
+};
 enum { MODE_STEP = 0, MODE_RESET = 1 };
 enum { DIR_STAY = 0, DIR_RIGHT = 1, DIR_LEFT = 2, DIR_UP = 3, DIR_DOWN = 4 };
 
@@ -97,6 +99,52 @@ __device__ __forceinline__ int bush_value_fast(const uint64_t* thr, int n, uint6
   int v = c - 2 + (t0 <= U ? 1 : 0) + (t1 <= U ? 1 : 0) + (t2 <= U ? 1 : 0);
   if (!(t0 <= U && t3 > U)) v = bush_value(thr, n, U);
   return v;
+}
+
+// ------------------------------------------------------------------------ keyed spawn sets
+// The wolves spawning among n tiles in a canonical order (the ring table, or view cells
+// c = i*H + j), iid Bernoulli(q) drawn by geometric gaps (oracle/keyed_rng.py spawn_hits):
+// the k-th draw (site 6, "tile" (k, 0)) gives G = #{g in 1..m : U < gap[g]} misses before
+// the next hit among the m tiles left.  The first draw ends the set at once iff U < gap[n]
+// (th, tl: gap[n] split), which at the default q = 0.0005 is 97.6 % of the ring draws: one
+// hash chain per env-step instead of one per ring tile.  `gap` (LDS or global) is only read
+// on a hit; hit(index) is called for each hit tile, ascending.
+__device__ __forceinline__ int gap_count(const uint64_t* gap, int m, uint64_t U) {
+  int g = 0;  // gap[0] = 2^53 > U; gap is non-increasing
+  for (int s = m > 0 ? 1 << (31 - __builtin_clz((uint32_t)m)) : 0; s; s >>= 1)
+    if (g + s <= m && U < gap[g + s]) g += s;
+  return g;
+}
+
+// The same count from a float guess: gap[g] ~ (1 - q)^g 2^53, so G = floor(log2(u) / log2(1 - q))
+// but within one of it near a boundary; gap[g] > U >= gap[g + 1] (one LDS round trip) proves
+// G = g, else the search decides.  inv_l2 = 1 / log2(1 - q) (< 0; q > 0 on this path).
+__device__ __forceinline__ int gap_count_fast(const uint64_t* gap, int m, uint64_t U, float inv_l2) {
+  const float u = (float)(uint32_t)(U >> 21) * 0x1p-32f;
+  const float gf = __builtin_amdgcn_logf(u) * inv_l2;  // u = 0: +inf
+  const int g = gf >= (float)m ? m : (int)gf;
+  const uint64_t a = gap[g], b = gap[min(g + 1, m)];
+  if (U < a && (g == m || U >= b)) return g;
+  return gap_count(gap, m, U);
+}
+
+template <typename Hit>
+__device__ __forceinline__ void spawn_hits(const uint64_t* gap, int n, uint32_t th, uint32_t tl, float inv_l2,
+                                           int32_t turn, uint32_t b0, uint32_t b1, Hit&& hit) {
+  const uint32_t ts = make_ts(SITE_GAP, 0, turn);
+  const uint32_t h1 = fmix32(b0);  // "tile" (0, 0)
+  const uint32_t hi = fmix32(h1 ^ ts ^ b1);
+  if (n <= 0 || !U_ge(h1, hi, ts, b0, th, tl)) return;
+  uint64_t U = ((uint64_t)hi << 21) | draw_lo21(h1, ts, b0);
+  int pos = 0;
+  for (uint32_t k = 1;; ++k) {
+    const int G = gap_count_fast(gap, n - pos, U, inv_l2);
+    if (G >= n - pos) break;
+    pos += G;
+    hit(pos);
+    if (++pos >= n) break;
+    U = draw_U(xy_pack((int32_t)(k & 0xFFFFu), (int32_t)(k >> 16)), ts, b0, b1);
+  }
 }
 
 // the pads of bush_value_fast's table around thr[0 .. n) (one lane)

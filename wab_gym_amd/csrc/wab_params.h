@@ -59,8 +59,15 @@ struct Params {
   // "U >= T" tests on 53-bit draws U = hi << 21 | lo21, split as (T >> 21, T & 0x1FFFFF);
   // T = 2^53 ("never") is encoded (0xFFFFFFFF, 0xFFFFFFFF) which no (hi, lo21) reaches
   uint32_t keep_th, keep_tl;    // despawn: wolf kept iff U >= keep_gt + 1  (u > p, wab_env.py:263)
-  uint32_t spawn_th, spawn_tl;  // spawn: wolf iff !(U >= spawn_lt)          (u < p/2, wab_env.py:573)
   uint32_t bush_th, bush_tl;    // bush present iff U >= T_1                 (wab_env.py:632-635)
+  // wolf spawns (u < p/2, wab_env.py:573, :590) are drawn as sets by geometric gaps
+  // (oracle/keyed_rng.py spawn_hits): gap[g] = floor((1 - q)^g 2^53), g = 0..n_gap; the
+  // first draw of a set is a miss of all n tiles iff U < gap[n], tested split like the above
+  const uint64_t* gap;          // device [n_gap + 1]
+  int32_t n_gap;                // max(R, WH)
+  float gap_inv_l2;             // 1 / log2(1 - q) (the guess of gap_count_fast; the table decides)
+  uint32_t gap_ring_th, gap_ring_tl;  // gap[R]: no spawn on the ring this turn
+  uint32_t gap_view_th, gap_view_tl;  // gap[WH]: no initial wolf in the view
   const uint64_t* thresholds;  // device [max_berries] T_k
   const uint32_t* tables;      // device: [WH] view-cell world offsets (cw - i, ch - j), then from
   int32_t ring_at;             //   ring_at (16-B aligned) the R ring offsets, padded to a multiple of 4
@@ -140,7 +147,7 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) 
 // LDS of the four-wave small-view step (wab_step_small.hip): one 64-env group per
 // workgroup (dwords)
 struct SmallLayout {
-  uint32_t tiles, thr, stream, stream_words, cval, flag, wolfp, kill, bushp, info, spawn, jbm, jwm, jkey;
+  uint32_t tiles, thr, gap, stream, stream_words, cval, flag, wolfp, kill, bushp, strip, gone, info, spawn, jbm, jkey;
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
 };
 
@@ -149,6 +156,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   uint32_t o = 0;
   L.tiles = o; o += lds_align4((uint32_t)p.WH);
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
+  L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.stream_words = lds_align4((64u * (uint32_t)p.OB + 31u) >> 5);
   L.stream = o; o += L.stream_words + 4u;  // + slack for stream_or128's fifth dword
   L.cval = o; o += 64u;
@@ -156,10 +164,11 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.wolfp = o; o += 64u * 4u;
   L.kill = o; o += 64u;
   L.bushp = o; o += 64u * 4u;
+  L.strip = o; o += 2u * 64u * 4u;
+  L.gone = o; o += 64u * 4u;
   L.info = o; o += 64u;
-  L.spawn = o; o += 4u * 64u * 4u;
+  L.spawn = o; o += 64u * 4u;
   L.jbm = o; o += 64u * 4u;
-  L.jwm = o; o += 64u * 4u;  // (directly after jbm: zeroed together)
   L.jkey = o; o += 2u * 2u * 64u;
   L.fbits = L.ftab = L.fzero = L.scal = o;
   if (p.features) {  // fused features: 64 envs x F bits (+ slack), the per-cell tables (zeroed
@@ -181,7 +190,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
 // different banks (dwords)
 constexpr uint32_t kWidePitch = 33;
 struct WideLayout {
-  uint32_t bm, wp, spawn, spw, ring, thr, cval, info, blk, jobEnv, jobKey, total;
+  uint32_t bm, wp, spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey, total;
 };
 
 __host__ __device__ inline WideLayout wide_layout(const Params& p) {
@@ -194,6 +203,7 @@ __host__ __device__ inline WideLayout wide_layout(const Params& p) {
   L.spw = (((uint32_t)p.R + 31u) >> 5) | 1u;  // spawn-mask dwords per env (odd pitch)
   L.spawn = o; o += lds_align4(64u * L.spw);
   L.ring = o; o += lds_align4((uint32_t)p.R);  // spawn-ring offsets
+  L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));  // spawn-set gap table
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.cval = o; o += 64u;                       // generated berries of the ostrich's tile
   L.info = o; o += 64u;                       // W0 -> all: job | emptied << 1

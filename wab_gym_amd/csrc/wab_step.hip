@@ -286,17 +286,12 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       if (be < n_active) {
         const uint4 sn = *reinterpret_cast<const uint4*>(&snap[be * 4]);
         const uint32_t kb0 = sn.y;
-        // spawn ring around the new position (spawn_wolves :527-576): wolf iff u < p/2
-        const uint32_t ts_spawn = make_ts(SITE_SPAWN, 0, (int32_t)(sn.w & 0xFFFFFu));
-        const uint32_t hk = ts_spawn ^ sn.z;
+        // spawn ring around the new position (spawn_wolves :527-576): the ring's spawn set
+        // this turn, one draw unless a wolf spawns (keyed spawn sets, wab_device.h)
         uint32_t* sm = spawnM + be * p.RW;
-#pragma unroll 2
-        for (int r = sub; r < p.R; r += G) {
-          const uint32_t h1 = fmix32(xy_add(sn.x, tiles[p.WH + r]) ^ kb0);
-          const uint32_t hi = fmix32(h1 ^ hk);
-          if (hi <= p.spawn_th && (hi < p.spawn_th || draw_lo21(h1, ts_spawn, kb0) < p.spawn_tl))
-            atomicOr(&sm[r >> 5], 1u << (r & 31));
-        }
+        if (sub == 0 && p.wolves_on)
+          spawn_hits(p.gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, (int32_t)(sn.w & 0xFFFFFu), kb0, sn.z,
+                     [&](int r) { atomicOr(&sm[r >> 5], 1u << (r & 31)); });
         // the row or column that scrolled into view (generate_bushes :613-629)
         const int bdir = (int)(sn.w >> 24);
         if (bdir != DIR_STAY) {
@@ -532,7 +527,15 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       const int items = n_jobs * WH;
       int ij = tid / WH, ic = tid - (tid / WH) * WH;
       const int stepJ = kThreads / WH, stepC = kThreads - (kThreads / WH) * WH;
-      const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), ts_wolf = make_ts(SITE_SPAWN, 0, 0);
+      const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
+      // initialize_wolves (:578-593): each job's view spawn set at turn 0, one thread per job
+      if (p.wolves_on && tid < n_jobs) {
+        const uint32_t je = jobEnv[tid];
+        spawn_hits(p.gap, WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, jobKey[2 * tid], jobKey[2 * tid + 1], [&](int c) {
+          lds_set(sB, je * (uint32_t)p.OB + tile_bit(tiles[c]));
+          lds_set(wolfM + tid * p.WHW, (uint32_t)c);
+        });
+      }
       for (int q = tid; q < items; q += kThreads) {
         const uint32_t je = jobEnv[ij], kb0 = jobKey[2 * ij], kb1 = jobKey[2 * ij + 1];
         const uint32_t t = tiles[ic];
@@ -541,13 +544,6 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
         const uint32_t hb = fmix32(h1 ^ ts_bush ^ kb1);
         if (U_ge(h1, hb, ts_bush, kb0, p.bush_th, p.bush_tl))         // generate_bushes
           atomicOr(&BM<NE>(bm, ic >> 5, (int)je), 1u << (ic & 31));
-        if (p.wolves_on) {                                               // initialize_wolves
-          const uint32_t hw = fmix32(h1 ^ ts_wolf ^ kb1);
-          if (!U_ge(h1, hw, ts_wolf, kb0, p.spawn_th, p.spawn_tl)) {
-            lds_set(sB, je * (uint32_t)p.OB + tile_bit(t));
-            lds_set(wolfM + ij * p.WHW, (uint32_t)ic);
-          }
-        }
         ic += stepC;
         ij += stepJ;
         if (ic >= WH) { ic -= WH; ij += 1; }

@@ -10,12 +10,12 @@
 // running an independent part of the step; they meet at LDS barriers:
 //
 //          W0 bushes             W1 draws              W2 wolves             W3 ring
-//   init   state + first eaten-  thresholds -> LDS     wolf slots, header    tile table -> LDS
-//          log loads
+//   init   state + first eaten-  thresholds -> LDS     wolf slots, header    tile + gap tables
+//          log loads                                                         -> LDS
 //   -- B_init --
-//   P0     scroll, entering      the ostrich tile's    despawn, pursuit,     ring [6/12, 1)
-//          row/col draws, log,   value (LDS flag),     wolf grid of S, kill,
-//          eat, hunger, starve   ring [0, 5/12)        ring [5/12, 6/12)
+//   P0     scroll, log, eat,     the ostrich tile's    despawn, pursuit,     the ring's spawn
+//          hunger, starve        value (LDS flag)      wolf grid of S, kill  set, entering
+//                                                                            row/column draws
 //   -- B1 --
 //   P1     status, reward,       reset draws (cells    spawns, wolf slots,   reset draws (the
 //          done, scalars,        0..63, LDS flag),     header                rest), new episodes
@@ -30,7 +30,8 @@
 // Every wave that needs "done" recomputes it from the flags handed over at B1 (starved from
 // W0, killed from W2), so no wave waits for another's bookkeeping.  Draws are batched four
 // at a time (fmix32x4) so dependent hash chains interleave; the rare threshold ties (high
-// 32 bits equal) are resolved in a separate branch.
+// 32 bits equal) are resolved in a separate branch.  Wolf spawns are keyed sets
+// (wab_device.h spawn_hits): one draw per env-step and per new episode unless a wolf spawns.
 #include <hip/hip_runtime.h>
 
 #include "wab_feat.h"
@@ -134,94 +135,48 @@ __host__ __device__ constexpr uint32_t ring11(int r) {
   return ((uint32_t)(xi - 6) & 0xFFFFu) | ((uint32_t)(yi - 6) << 16);
 }
 
-// spawn draws (spawn_wolves :527-576, wolf iff u < p/2) on ring tiles [r0, r1), r0 % 4 == 0
-template <int G>
-__device__ __forceinline__ void ring_part(const Params& p, const Head& h, uint32_t b0, uint32_t b1, int r0, int r1,
-                                          M128& spawn) {
-  const uint32_t ts = make_ts(SITE_SPAWN, 0, h.turn), hk = ts ^ b1;
-  const uint4* ring = reinterpret_cast<const uint4*>(p.tables + p.ring_at);  // uniform: scalar loads
-  constexpr int kUnroll = G == 11 ? 16 : 1;
-#pragma unroll kUnroll
-  for (int r = r0; r < r1; r += 4) {
-    // padded to a multiple of 4 entries
-    const uint4 o = G == 11 ? make_uint4(ring11(r), ring11(r + 1), ring11(r + 2), ring11(r + 3)) : ring[r >> 2];
-    uint32_t h1[4] = {xy_add(h.cpos, o.x) ^ b0, xy_add(h.cpos, o.y) ^ b0, xy_add(h.cpos, o.z) ^ b0,
-                      xy_add(h.cpos, o.w) ^ b0};
-    fmix32x4(h1);
-    uint32_t hh[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) hh[k] = h1[k] ^ hk;
-    fmix32x4(hh);
-    uint32_t hits = 0, tie = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      hits |= (hh[k] < p.spawn_th ? 1u : 0u) << k;
-      tie |= (hh[k] == p.spawn_th ? 1u : 0u) << k;
-    }
-    if (tie) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, b0) < p.spawn_tl) hits |= 1u << k;
-    }
-    hits &= r + 4 <= r1 ? 0xFu : (1u << (r1 - r)) - 1u;
-    if (r < 64) spawn.lo |= (uint64_t)hits << r;  // r is a multiple of 4: no straddle
-    else spawn.hi |= (uint64_t)hits << (r - 64);
-  }
-}
-
-// the spawn ring split in twelfths (multiples of 4), balanced against each wave's other work
-// before B1: W1 [0, 5/12), W2 [5/12, 6/12), W3 [6/12, 1); none on W0, the longest chain
-// (A/B at B = 65536, tools/ab.sh: 2/12-4/12-6/12 11.65 us, this split 11.27 us, with W1's
-// reset draws ahead of its render)
-__device__ __forceinline__ int ring_cut(const Params& p, int k) { return min(p.R, ((p.R * k / 12) + 3) & ~3); }
-
-// reset draws (generate_bushes, initialize_wolves) of every job for view cells
-// c = c0 + lane, into the jobs' bush / wolf bitmaps
+// reset draws (generate_bushes) of every job for view cells c = c0 + lane, into the jobs'
+// bush bitmaps (the initial wolves are a spawn set: new_episode)
 __device__ __forceinline__ void reset_chunk(const Params& p, const uint32_t* tiles, const uint32_t* jkey, int n_jobs,
-                                            uint32_t c0, int lane, uint32_t* jbm, uint32_t* jwm) {
+                                            uint32_t c0, int lane, uint32_t* jbm) {
   const uint32_t WH = (uint32_t)p.WH;
   const uint32_t c = c0 + (uint32_t)lane;
   const uint32_t xy = c < WH ? tiles[c] : 0u;  // ostrich at (0, 0)
-  const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), ts_wolf = make_ts(SITE_SPAWN, 0, 0);
+  const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
   for (int j4 = 0; j4 < n_jobs; j4 += 4) {
-    uint32_t kb0[4], kb1[4], h1[4], hb[4], hw[4];
+    uint32_t kb0[4], h1[4], hb[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint2 kq = *reinterpret_cast<const uint2*>(&jkey[2 * min(j4 + q, n_jobs - 1)]);
       kb0[q] = kq.x;
-      kb1[q] = kq.y;
       h1[q] = xy ^ kq.x;
+      hb[q] = ts_bush ^ kq.y;
     }
     fmix32x4(h1);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      hb[q] = h1[q] ^ ts_bush ^ kb1[q];
-      hw[q] = h1[q] ^ ts_wolf ^ kb1[q];
-    }
+    for (int q = 0; q < 4; ++q) hb[q] ^= h1[q];
     fmix32x4(hb);
-    fmix32x4(hw);
     if (c < WH) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (j4 + q >= n_jobs) break;
-        const int jj = j4 + q;
-        if (U_ge(h1[q], hb[q], ts_bush, kb0[q], p.bush_th, p.bush_tl)) atomicOr(&jbm[jj * 4 + (c >> 5)], 1u << (c & 31));
-        if (p.wolves_on && !U_ge(h1[q], hw[q], ts_wolf, kb0[q], p.spawn_th, p.spawn_tl))
-          atomicOr(&jwm[jj * 4 + (c >> 5)], 1u << (c & 31));
+        if (U_ge(h1[q], hb[q], ts_bush, kb0[q], p.bush_th, p.bush_tl))
+          atomicOr(&jbm[(j4 + q) * 4 + (c >> 5)], 1u << (c & 31));
       }
     }
   }
 }
 
-// the row or column that scrolled into view (generate_bushes :613-629): its bush bits
-__device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint32_t b0, uint32_t b1) {
+// the row or column that scrolled into view (generate_bushes :613-629): the bush bits of its
+// cells [c0, c1) (multiples of 4)
+__device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint32_t b0, uint32_t b1, int c0, int c1) {
   M128 nb = {0ull, 0ull};
   if (h.dir != DIR_STAY) {
     const bool horiz = h.dir == DIR_RIGHT || h.dir == DIR_LEFT;
     const int n = horiz ? p.H : p.W;
     const int i0 = h.dir == DIR_LEFT ? p.W - 1 : 0, j0 = h.dir == DIR_DOWN ? p.H - 1 : 0;
     const uint32_t ts = make_ts(SITE_BUSH, 0, 0), hk = ts ^ b1;
-    for (int c = 0; c < p.SL; c += 4) {
+    for (int c = c0; c < min(c1, p.SL); c += 4) {
       uint32_t h1[4], hh[4], cb[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -256,16 +211,18 @@ __device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint
 struct Lds {
   uint32_t* tiles;  // [WH] view-cell world offsets (reset draws, initial wolves)
   uint64_t* thr;    // [max_berries] bush thresholds (W1), padded (bush_thr_pads)
+  uint64_t* gap;    // [n_gap + 1] spawn-set gap table (W3; read on a hit only)
   uint32_t* stream; // 64 envs x OB bits: bit k = byte k of the group's obs chunk
   uint32_t* cval;   // [64] generated berries of the ostrich's tile (W1), then flag[0] = 1
   uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done; zeroed by W0 before B_init
   uint4* wolfp;     // [64] wolf grid of S (W2, P0)
   uint32_t* kill;   // [64] (W2, P0)
-  uint4* bushp;     // [64] bush grid of S (W0, P0)
+  uint4* bushp;     // [64] bush grid of S without the entering strip (W0, P0)
+  uint4* strip;     // [2][64] bush bits of the strip that scrolled into view (W1, W3; P0)
+  uint4* gone;      // [64] emptied tiles in view (W0, P0): cleared from the strip too
   uint32_t* info;   // [64] starved | role << 8 | eaten << 16 | emptied << 24 (W0, P0)
-  uint4* spawn;     // [3][64] ring spawn masks (W1, W2, W3)
+  uint4* spawn;     // [64] ring spawn sets (W3)
   uint32_t* jbm;    // [job][4] reset bush bitmaps (W1, W3)
-  uint32_t* jwm;    // [job][4] reset wolf cells (W1, W3)
   uint32_t* jkey;   // [2][job][2] the new episodes' keys: W1's copy, W3's copy
   uint32_t* scal;   // [64] fused features: food_turns | role << 8 | status << 16 of the obs
 };
@@ -274,22 +231,34 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   Lds s;
   s.tiles = lds + L.tiles;
   s.thr = reinterpret_cast<uint64_t*>(lds + L.thr) + 1;
+  s.gap = reinterpret_cast<uint64_t*>(lds + L.gap);
   s.stream = lds + L.stream;
   s.cval = lds + L.cval;
   s.flag = lds + L.flag;
   s.wolfp = reinterpret_cast<uint4*>(lds + L.wolfp);
   s.kill = lds + L.kill;
   s.bushp = reinterpret_cast<uint4*>(lds + L.bushp);
+  s.strip = reinterpret_cast<uint4*>(lds + L.strip);
+  s.gone = reinterpret_cast<uint4*>(lds + L.gone);
   s.info = lds + L.info;
   s.spawn = reinterpret_cast<uint4*>(lds + L.spawn);
   s.jbm = lds + L.jbm;
-  s.jwm = lds + L.jwm;
   s.jkey = lds + L.jkey;
   s.scal = lds + L.scal;
   return s;
 }
 
 __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u; }
+
+// the entering strip's cells are drawn in two parts, [0, kStripW1) on W1 after the tile value
+// and the rest on W3 after the spawn set (A/B: -DWAB_STRIP_W1=k)
+#ifndef WAB_STRIP_W1
+#define WAB_STRIP_W1 8
+#endif
+constexpr int kStripW1 = WAB_STRIP_W1;
+__device__ __forceinline__ M128 strip_of(const Lds& s, int lane) {
+  return m_or(m_unpack(s.strip[lane]), m_unpack(s.strip[64 + lane]));
+}
 
 // scan eaten-log entries [i0, i0 + 4): the entry on the ostrich's tile, and the emptied
 // tiles in view (absent from S, :506)
@@ -310,7 +279,8 @@ __device__ __forceinline__ void scan_log(const Params& p, const Head& h, const u
 }
 
 // The new episode of a done env (reset :231-248, spawn_ostriches :595-611): state, scalars,
-// initial wolves, and its obs segment (which must be clear) from the job's reset draws.
+// initial wolves (initialize_wolves :578-593: the view's spawn set at turn 0), and its obs
+// segment (which must be clear) from the job's reset draws.
 template <int SLOTS>
 __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const Head& h, int64_t g, int j,
                                             uint32_t ebit, unsigned long long& wolf_of) {
@@ -324,7 +294,9 @@ __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const
                         ? (int)(draw_U(xy_pack(0, 0), make_ts(SITE_START_ROLE, 0, 0), kb0, kb1) >> 52)
                         : p.start_role;
   const M128 nbm = m_unpack(*reinterpret_cast<const uint4*>(&s.jbm[4 * j]));
-  const M128 nwm = m_unpack(*reinterpret_cast<const uint4*>(&s.jwm[4 * j]));
+  M128 nwm = {0ull, 0ull};
+  if (p.wolves_on)
+    spawn_hits(s.gap, p.WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, kb0, kb1, [&](int c) { m_set(nwm, (uint32_t)c); });
   M128 ost = {0ull, 0ull}, wp = nwm, bp = nbm;
   m_set(ost, ccb);
   if (p.restrict_view) {
@@ -426,20 +398,16 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
                        sel64(up, col0.hi, 0ull) | sel64(down, coll.hi, 0ull)};
     bm = m_andn(m_and(bm, valid), drop);
   }
-  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
-  const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
   SMALL_STAMP(1);
-  bm = m_or(bm, strip_draws(p, h, b0, b1));
   SMALL_STAMP(2);
   // eaten log: the berries left on the ostrich's tile, and emptied tiles that scrolled back
   // into view (absent from S, :506); the first entries whatever the tile holds (clearing an
-  // emptied tile that is already absent changes nothing), the rest when it can matter
+  // emptied tile that is already absent changes nothing), the rest when it can matter.  The
+  // entering strip (W3) never holds the ostrich's tile; `gone` clears it where it is read.
   int found = -1, found_rem = 0;
-  {
-    M128 gone = {0ull, 0ull};
-    scan_log(p, h, lxy, lrem, 0, ne, found, found_rem, gone);
-    bm = m_andn(bm, gone);
-  }
+  M128 gone = {0ull, 0ull};
+  scan_log(p, h, lxy, lrem, 0, ne, found, found_rem, gone);
+  bm = m_andn(bm, gone);
   bool center_bush = m_test(bm, ccb);
   if (ne > 4 && (center_bush || (ndep > 0 && h.dir != DIR_STAY))) {
     for (int i0 = 4; i0 < ne; i0 += 4) {
@@ -449,14 +417,14 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
           lxy[k] = p.eaten_xy[(int64_t)(i0 + k) * p.B + g];
           lrem[k] = p.eaten_rem[(int64_t)(i0 + k) * p.B + g];
         }
-      M128 gone = {0ull, 0ull};
       scan_log(p, h, lxy, lrem, i0, ne, found, found_rem, gone);
-      bm = m_andn(bm, gone);
     }
+    bm = m_andn(bm, gone);
     center_bush = m_test(bm, ccb);
   }
   SMALL_STAMP(7);
-  s.bushp[lane] = m_pack(bm);  // bush grid of S (pre-eat)
+  s.bushp[lane] = m_pack(bm);  // bush grid of S (pre-eat) but the strip
+  s.gone[lane] = m_pack(gone);
   int rem = found_rem;         // berries left: the log, else the generated value (W1)
   if (found < 0) {
     rem = 0;
@@ -521,6 +489,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
     }
     if (p.features && !job) s.scal[lane] = (uint32_t)ft | ((uint32_t)role << 8) | ((uint32_t)status << 16);
     if (!job) {
+      bm = m_or(bm, m_andn(strip_of(s, lane), gone));
       p.bushmap[g] = m_word<0>(bm);
       if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(bm);
       if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(bm);
@@ -592,10 +561,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   if (p.features && !p.restrict_view)  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
   SMALL_STAMP(11);
-  // spawn ring part W1
-  M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, 0, ring_cut(p, 5), spawn);
-  s.spawn[lane] = m_pack(spawn);
+  s.strip[lane] = m_pack(strip_draws(p, h, b0, b1, 0, kStripW1));  // generate_bushes (:613-629): the entering strip
   SMALL_STAMP(12);
   lds_barrier();  // B1
   const uint32_t info = s.info[lane];
@@ -607,7 +573,8 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
     const uint32_t ebit = (uint32_t)lane * OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
     M128 ost = {0ull, 0ull};
     m_set(ost, ccb);
-    M128 wp = m_unpack(s.wolfp[lane]), bp = m_unpack(s.bushp[lane]);
+    M128 wp = m_unpack(s.wolfp[lane]);
+    M128 bp = m_or(m_unpack(s.bushp[lane]), m_andn(strip_of(s, lane), m_unpack(s.gone[lane])));
     if (p.restrict_view) {  // mask_grid (:344-357) by the fresh role
       const M128 vm = view_mask_of(p, (int)((info >> 8) & 0xFFu));
       wp = m_andn(wp, vm);
@@ -628,7 +595,7 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
       const int j = __popcll(jm & ((1ull << lane) - 1ull));
       *reinterpret_cast<uint2*>(&s.jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
     }
-    reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm, s.jwm);
+    reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm);
     lds_publish(&s.flag[1]);
   }
   render();
@@ -732,16 +699,12 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   s.wolfp[lane] = m_pack(wolfp);
   s.kill[lane] = kill ? 1u : 0u;
   SMALL_STAMP(17);
-  // ring part B
-  M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 5), ring_cut(p, 6), spawn);
-  s.spawn[64 + lane] = m_pack(spawn);
   SMALL_STAMP(18);
-  lds_barrier();  // B1: every ring part, the starve flags and the bushes' counts are in
+  lds_barrier();  // B1: the spawn set, the starve flags and the bushes' counts are in
 
   // spawn_wolves (:325-326): new wolves into free slots (outside the view, not in S)
   unsigned long long wolf_of = 0;
-  spawn = m_or(m_or(m_unpack(s.spawn[lane]), m_unpack(s.spawn[64 + lane])), m_unpack(s.spawn[128 + lane]));
+  const M128 spawn = m_unpack(s.spawn[lane]);
   if (active && (spawn.lo | spawn.hi)) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -798,9 +761,15 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
     for (int k = 0; k < 2; ++k)
       if (64 * k + lane < p.WH) s.tiles[64 * k + lane] = tv[k];
   }
-  {  // zero the reset tables (jbm, jwm: [64][4] each, contiguous)
-    uint4* z = reinterpret_cast<uint4*>(s.jbm);
-    for (int i = lane; i < 2 * 64; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  reinterpret_cast<uint4*>(s.jbm)[lane] = make_uint4(0u, 0u, 0u, 0u);  // reset bitmaps [64][4]
+  {  // the spawn sets' gap table, every load in flight at once
+    const int n = p.n_gap + 1;  // <= 129
+    uint64_t gv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gv[k] = p.gap[min(64 * k + lane, n - 1)];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if (64 * k + lane < n) s.gap[64 * k + lane] = gv[k];
   }
   if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned)
     uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
@@ -814,10 +783,12 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
   }
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
-  // ring part C
+  // spawn_wolves (:527-576): the ring's spawn set this turn (one draw unless a wolf spawns)
   M128 spawn = {0ull, 0ull};
-  if (p.wolves_on) ring_part<G>(p, h, b0, b1, ring_cut(p, 6), p.R, spawn);
-  s.spawn[128 + lane] = m_pack(spawn);
+  if (p.wolves_on && h.active)
+    spawn_hits(s.gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, b0, b1, [&](int r) { m_set(spawn, (uint32_t)r); });
+  s.spawn[lane] = m_pack(spawn);
+  s.strip[64 + lane] = m_pack(strip_draws(p, h, b0, b1, kStripW1, 1 << 30));  // the entering strip, part 2
   SMALL_STAMP(23);
   lds_barrier();  // B1
   // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
@@ -833,7 +804,7 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
     }
     const int n_jobs = __popcll(jm);
     for (uint32_t c0 = 64; c0 < (uint32_t)p.WH; c0 += 64)  // cells [0, 64): W1
-      reset_chunk(p, s.tiles, jkey, n_jobs, c0, lane, s.jbm, s.jwm);
+      reset_chunk(p, s.tiles, jkey, n_jobs, c0, lane, s.jbm);
     if (!p.t_planes) {
       lds_await(p, &s.flag[1]);  // W1's part of the draws
       unsigned long long wolf_of = 0;

@@ -7,15 +7,15 @@
 // workgroup serves 64 envs; each wave runs one lane per env:
 //
 //          W0 dynamics            W1 bushes               W2 ring         W3
-//   P0     state + log loads,     bitmap rows (one dword  ring offsets    ostrich grids
-//          despawn, pursuit,      per row), scroll,       -> LDS, first   -> obs plane 2
-//          kill, wolf grids of S  entering row/column     spawn-ring      (first half)
-//          -> obs plane 0         draws, emptied tiles,   word; ostrich
+//   P0     state + log loads,     bitmap rows (one dword  ring offsets,   ostrich grids
+//          despawn, pursuit,      per row), scroll,       gap table ->    -> obs plane 2
+//          kill, wolf grids of S  entering row/column     LDS, the spawn  (first half)
+//          -> obs plane 0         draws, emptied tiles,   set; ostrich
 //                                 ostrich-tile value      grids (second
 //                                                         half)
 //   -- B1 --  S (the obs snapshot) is complete
-//   P1     eat, hunger, starve,   obs plane 1 (bushes)    obs plane 1     the rest of
-//          reward/done, scalars,                                          the ring
+//   P1     eat, hunger, starve,   obs plane 1 (bushes)    obs plane 1
+//          reward/done, scalars,
 //          job list; obs plane 1
 //   -- B2 --
 //   P2     W0: spawns, state stores; all: post-eat bitmaps, terminal obs of done envs
@@ -128,40 +128,6 @@ __device__ __forceinline__ uint32_t strip_bits(const Params& p, const WHead& h) 
         if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, h.b0) >= p.bush_tl) hit |= 1u << k;
     }
     bits |= (hit & in) << c;
-  }
-  return bits;
-}
-
-// spawn draws (spawn_wolves :527-576, wolf iff u < p/2) of ring tiles [32 w, 32 w + 32);
-// the ring offsets come from the LDS copy (a scalar load from L2 stalls for microseconds
-// once the obs stores are streaming)
-__device__ __forceinline__ uint32_t ring_word(const Params& p, const WHead& h, const uint32_t* ring_lds, int w) {
-  const int r0 = 32 * w, r1 = min(p.R, r0 + 32);
-  const uint32_t ts = make_ts(SITE_SPAWN, 0, h.turn), hk = ts ^ h.b1;
-  const uint4* ring = reinterpret_cast<const uint4*>(ring_lds);
-  uint32_t bits = 0;
-  for (int r = r0; r < r1; r += 4) {
-    const uint4 o = ring[r >> 2];  // padded to a multiple of 4 entries (broadcast read)
-    uint32_t h1[4] = {xy_add(h.cpos, o.x) ^ h.b0, xy_add(h.cpos, o.y) ^ h.b0, xy_add(h.cpos, o.z) ^ h.b0,
-                      xy_add(h.cpos, o.w) ^ h.b0};
-    fmix32x4(h1);
-    uint32_t hh[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) hh[k] = h1[k] ^ hk;
-    fmix32x4(hh);
-    uint32_t hits = 0, tie = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      hits |= (hh[k] < p.spawn_th ? 1u : 0u) << k;
-      tie |= (hh[k] == p.spawn_th ? 1u : 0u) << k;
-    }
-    if (tie) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, h.b0) < p.spawn_tl) hits |= 1u << k;
-    }
-    hits &= r + 4 <= r1 ? 0xFu : (1u << (r1 - r)) - 1u;
-    bits |= hits << (r - r0);
   }
   return bits;
 }
@@ -294,6 +260,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   uint32_t* wp = lds + L.wp;
   uint32_t* spawn = lds + L.spawn;
   uint32_t* ring = lds + L.ring;
+  uint64_t* gap = reinterpret_cast<uint64_t*>(lds + L.gap);  // (MODE_STEP; resets read p.gap)
   uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr) + 1;  // padded (bush_thr_pads)
   uint32_t* cval = lds + L.cval;
   uint32_t* info = lds + L.info;
@@ -305,7 +272,6 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   const uint32_t me = (uint32_t)lane * P;
   uint8_t* out = p.planes + (size_t)g0 * OB;
   const int RW = (p.R + 31) >> 5;                 // spawn-ring words
-  const int nA = p.wolves_on ? min(RW, 1) : 0;    // words drawn before B1 (W2); the rest: W3 after B1
 
   const WHead h = whead<MODE>(p, g, active);
 
@@ -595,30 +561,30 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         setprio_age(p);
       } else {
         // ---------------------------------------------- W3 P0: the ostrich grids; W2 P0: ring
-        // offsets -> LDS, first ring word
+        // offsets and gap table -> LDS, the spawn set (spawn_wolves :527-576)
         setprio_age(p);
         // the ostrich grids in two halves: W3 from the start, W2 after its ring word (it would
         // otherwise wait ~10 us at B1 while W3 alone issues them: 46.9 -> 46.3 us)
         if (wave == 3) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
         if (wave == 2) {
           copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
+          if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);  // (initial wolves: gap[WH])
+          for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
-          for (int w = 0; w < nA; ++w)
-            spawn[(uint32_t)lane * L.spw + (uint32_t)w] = active ? ring_word(p, h, ring, w) : 0u;
+          if (p.wolves_on && active)  // one draw unless a wolf spawns
+            spawn_hits(gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
+              spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
+            });
           obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
         }
       }
       WIDE_STAMP(8 * wave + 1);
       lds_barrier();  // B1
       WIDE_STAMP(8 * wave + 2);
-      // ------------------------------------------------ P1: W1, W2 obs of S; W3 the rest of the
-      // ring (its VALU work on its own SIMD overlaps the drain of the stores)
+      // ------------------------------------------------ P1: W1, W2 obs of S
       if (wave < 3) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       WIDE_STAMP(8 * wave + 3);
-      if (wave == 3 && p.wolves_on)
-        for (int w = nA; w < RW; ++w)
-          spawn[(uint32_t)lane * L.spw + (uint32_t)w] = active ? ring_word(p, h, ring, w) : 0u;
       WIDE_STAMP(8 * wave + 4);
       lds_barrier();  // B2
       WIDE_STAMP(8 * wave + 5);
@@ -671,9 +637,10 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   if (n_jobs > 0) {
     // ------------------------------------------------ done envs: new episodes (:231-248)
     if (MODE == MODE_STEP) lds_barrier();  // B3: the snapshot rows of the jobs are read
-    // reset draws (generate_bushes, initialize_wolves) over the new view, ostrich at (0, 0):
-    // 32 lanes per row, rows written by ballot
-    const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0), ts_wolf = make_ts(SITE_SPAWN, 0, 0);
+    // reset draws (generate_bushes) over the new view, ostrich at (0, 0): 32 lanes per row,
+    // rows written by ballot; initialize_wolves (:578-593): the view's spawn set at turn 0, by
+    // the job's own lane of W0
+    const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
     const uint32_t rows2 = ((uint32_t)p.W + 1u) >> 1;  // wave-units of two rows
     for (int jj = 0; jj < n_jobs; ++jj) {
       const uint32_t e = jobEnv[jj];
@@ -685,17 +652,19 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         const uint32_t h1 = fmix32(xy ^ kq.x);
         const uint32_t hb = fmix32(h1 ^ ts_bush ^ kq.y);
         const bool bush = cell && U_ge(h1, hb, ts_bush, kq.x, p.bush_th, p.bush_tl);
-        bool wolf = false;
-        if (p.wolves_on) {
-          const uint32_t hw = fmix32(h1 ^ ts_wolf ^ kq.y);
-          wolf = cell && !U_ge(h1, hw, ts_wolf, kq.x, p.spawn_th, p.spawn_tl);
-        }
-        const unsigned long long bb = __ballot(bush), bw = __ballot(wolf);
-        if ((lane & 31) == 0 && i < (uint32_t)p.W) {
-          bm[e * P + i] = (uint32_t)(lane ? bb >> 32 : bb);
-          wp[e * P + i] = (uint32_t)(lane ? bw >> 32 : bw);
-        }
+        const unsigned long long bb = __ballot(bush);
+        if ((lane & 31) == 0 && i < (uint32_t)p.W) bm[e * P + i] = (uint32_t)(lane ? bb >> 32 : bb);
       }
+    }
+    if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
+      const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
+      for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;
+      if (p.wolves_on)
+        spawn_hits(MODE == MODE_STEP ? gap : p.gap, p.WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, (uint32_t)ek2,
+                   (uint32_t)(ek2 >> 32), [&](int c) {
+                     const uint32_t i = (uint32_t)c / (uint32_t)p.H;
+                     wp[me + i] |= 1u << ((uint32_t)c - i * (uint32_t)p.H);
+                   });
     }
     lds_barrier();  // B4
     if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
