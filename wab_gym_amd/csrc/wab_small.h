@@ -59,20 +59,22 @@ __device__ __forceinline__ void stream_clear(uint32_t* s, uint32_t at, uint32_t 
   }
 }
 
-// four independent fmix32 chains, written step-interleaved so that a single wave issues
-// them back to back (ILP) instead of waiting on each dependent result
-__device__ __forceinline__ void fmix32x4(uint32_t h[4]) {
+// K independent fmix32 chains, written step-interleaved so that a single wave issues them
+// back to back (ILP) instead of waiting on each dependent result
+template <int K>
+__device__ __forceinline__ void fmix32xk(uint32_t h[K]) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) h[k] ^= h[k] >> 16;
+  for (int k = 0; k < K; ++k) h[k] ^= h[k] >> 16;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) h[k] *= 0x85EBCA6Bu;
+  for (int k = 0; k < K; ++k) h[k] *= 0x85EBCA6Bu;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) h[k] ^= h[k] >> 13;
+  for (int k = 0; k < K; ++k) h[k] ^= h[k] >> 13;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) h[k] *= 0xC2B2AE35u;
+  for (int k = 0; k < K; ++k) h[k] *= 0xC2B2AE35u;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) h[k] ^= h[k] >> 16;
+  for (int k = 0; k < K; ++k) h[k] ^= h[k] >> 16;
 }
+__device__ __forceinline__ void fmix32x4(uint32_t h[4]) { fmix32xk<4>(h); }
 
 __device__ __forceinline__ M128 view_mask_of(const Params& p, int role) {
   const bool g = role == 1;

@@ -135,36 +135,45 @@ __host__ __device__ constexpr uint32_t ring11(int r) {
   return ((uint32_t)(xi - 6) & 0xFFFFu) | ((uint32_t)(yi - 6) << 16);
 }
 
+// reset draws (generate_bushes) of jobs [j0, j0 + K) for view cell c (xy its world offset)
+template <int K>
+__device__ __forceinline__ void reset_draws(const Params& p, const uint32_t* jkey, int j0, uint32_t xy, uint32_t c,
+                                            uint32_t* jbm) {
+  const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
+  uint32_t kb0[K], h1[K], hb[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    const uint2 kq = *reinterpret_cast<const uint2*>(&jkey[2 * (j0 + q)]);
+    kb0[q] = kq.x;
+    h1[q] = xy ^ kq.x;
+    hb[q] = ts_bush ^ kq.y;
+  }
+  fmix32xk<K>(h1);
+#pragma unroll
+  for (int q = 0; q < K; ++q) hb[q] ^= h1[q];
+  fmix32xk<K>(hb);
+  if (c < (uint32_t)p.WH) {
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+      if (U_ge(h1[q], hb[q], ts_bush, kb0[q], p.bush_th, p.bush_tl))
+        atomicOr(&jbm[(j0 + q) * 4 + (c >> 5)], 1u << (c & 31));
+  }
+}
+
 // reset draws (generate_bushes) of every job for view cells c = c0 + lane, into the jobs'
-// bush bitmaps (the initial wolves are a spawn set: new_episode)
+// bush bitmaps (the initial wolves are a spawn set: new_episode); jobs four, then two, then
+// one at a time (a group has 1.6 jobs on average: no draw is made for a job that is absent)
 __device__ __forceinline__ void reset_chunk(const Params& p, const uint32_t* tiles, const uint32_t* jkey, int n_jobs,
                                             uint32_t c0, int lane, uint32_t* jbm) {
-  const uint32_t WH = (uint32_t)p.WH;
   const uint32_t c = c0 + (uint32_t)lane;
-  const uint32_t xy = c < WH ? tiles[c] : 0u;  // ostrich at (0, 0)
-  const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
-  for (int j4 = 0; j4 < n_jobs; j4 += 4) {
-    uint32_t kb0[4], h1[4], hb[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint2 kq = *reinterpret_cast<const uint2*>(&jkey[2 * min(j4 + q, n_jobs - 1)]);
-      kb0[q] = kq.x;
-      h1[q] = xy ^ kq.x;
-      hb[q] = ts_bush ^ kq.y;
-    }
-    fmix32x4(h1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) hb[q] ^= h1[q];
-    fmix32x4(hb);
-    if (c < WH) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (j4 + q >= n_jobs) break;
-        if (U_ge(h1[q], hb[q], ts_bush, kb0[q], p.bush_th, p.bush_tl))
-          atomicOr(&jbm[(j4 + q) * 4 + (c >> 5)], 1u << (c & 31));
-      }
-    }
+  const uint32_t xy = c < (uint32_t)p.WH ? tiles[c] : 0u;  // ostrich at (0, 0)
+  int j = 0;
+  for (; j + 4 <= n_jobs; j += 4) reset_draws<4>(p, jkey, j, xy, c, jbm);
+  if (n_jobs - j >= 2) {
+    reset_draws<2>(p, jkey, j, xy, c, jbm);
+    j += 2;
   }
+  if (n_jobs - j == 1) reset_draws<1>(p, jkey, j, xy, c, jbm);
 }
 
 // the row or column that scrolled into view (generate_bushes :613-629): the bush bits of its
@@ -214,7 +223,8 @@ struct Lds {
   uint64_t* gap;    // [n_gap + 1] spawn-set gap table (W3; read on a hit only)
   uint32_t* stream; // 64 envs x OB bits: bit k = byte k of the group's obs chunk
   uint32_t* cval;   // [64] generated berries of the ostrich's tile (W1), then flag[0] = 1
-  uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done; zeroed by W0 before B_init
+  uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done, [2] S rendered (W2,
+                    // early obs stores); zeroed by W0 before B_init
   uint4* wolfp;     // [64] wolf grid of S (W2, P0)
   uint32_t* kill;   // [64] (W2, P0)
   uint4* bushp;     // [64] bush grid of S without the entering strip (W0, P0)
@@ -278,6 +288,62 @@ __device__ __forceinline__ void scan_log(const Params& p, const Head& h, const u
   }
 }
 
+// render S (:393-444) of one env into the bit-stream: the wolf grid (W2), the bush grid (W0,
+// plus the entering strip, W1/W3, minus emptied tiles), the ostrich; mask_grid (:344-357) by
+// the fresh role
+__device__ __forceinline__ void render_s(const Params& p, const Lds& s, int lane, uint32_t info) {
+  const uint32_t WH = (uint32_t)p.WH;
+  const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
+  M128 ost = {0ull, 0ull};
+  m_set(ost, ccb);
+  M128 wp = m_unpack(s.wolfp[lane]);
+  M128 bp = m_or(m_unpack(s.bushp[lane]), m_andn(strip_of(s, lane), m_unpack(s.gone[lane])));
+  if (p.restrict_view) {
+    const M128 vm = view_mask_of(p, (int)((info >> 8) & 0xFFu));
+    wp = m_andn(wp, vm);
+    bp = m_andn(bp, vm);
+    ost = m_andn(ost, vm);
+  }
+  stream_or128(s.stream, ebit, wp);
+  stream_or128(s.stream, ebit + WH, bp);
+  stream_or128(s.stream, ebit + 2 * WH, ost);
+}
+
+// Early obs stores (plain steps of full groups: no terminal obs, no fused features): the
+// group's obs chunk as 16-byte units (one 16-bit stream unit each), split by whether a unit
+// touches a done env.  Those that do not are final once S is rendered: W0, W1 and W2 store
+// them right after B1 (each wave-instruction 64 consecutive units, 1 KiB) while W3 builds the
+// new episodes; the rest go out after B2.  Every unit is stored exactly once.
+// Measured slower (10.34 -> 12.02 us at B = 65536: the stores of all groups then share the
+// HBM while W0-W2 still have to reach B2), so off unless built with -DWAB_EARLY_OBS=1.
+#ifndef WAB_EARLY_OBS
+#define WAB_EARLY_OBS 0
+#endif
+__device__ __forceinline__ bool early_obs(const Params& p) {
+  return WAB_EARLY_OBS && p.features == nullptr && p.t_planes == nullptr && (int64_t)blockIdx.x * 64 + 64 <= p.B;
+}
+
+__device__ __forceinline__ void store_unit(uint8_t* out, const uint32_t* stream, uint32_t u) {
+  const uint32_t v = reinterpret_cast<const uint16_t*>(stream)[u];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 q;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+  __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
+}
+
+// units [64 k + lane] for k = first, first + stride, ... that touch a done env iff `touching`
+__device__ __forceinline__ void store_units(const Params& p, const uint32_t* stream, unsigned long long jm,
+                                            bool touching, int first, int stride, int lane) {
+  const uint32_t OB = (uint32_t)p.OB, full = (64u * OB) >> 4;
+  uint8_t* out = p.planes + (size_t)blockIdx.x * 64u * OB;
+  for (uint32_t u = 64u * (uint32_t)first + (uint32_t)lane; u < full; u += 64u * (uint32_t)stride) {
+    const uint32_t e0 = (16u * u) / OB, e1 = (16u * u + 15u) / OB;
+    const bool t = (((jm >> e0) | (jm >> e1)) & 1ull) != 0ull;
+    if (t == touching) store_unit(out, stream, u);
+  }
+}
+
 // The new episode of a done env (reset :231-248, spawn_ostriches :595-611): state, scalars,
 // initial wolves (initialize_wolves :578-593: the view's spawn set at turn 0), and its obs
 // segment (which must be clear) from the job's reset draws.
@@ -285,8 +351,8 @@ template <int SLOTS>
 __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const Head& h, int64_t g, int j,
                                             uint32_t ebit, unsigned long long& wolf_of) {
   const uint32_t WH = (uint32_t)p.WH, ccb = (uint32_t)(p.cw * p.H + p.ch);
-  const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
-  const uint32_t kb0 = (uint32_t)ek2, kb1 = (uint32_t)(ek2 >> 32);
+  const uint2 kq = *reinterpret_cast<const uint2*>(&s.jkey[2 * j]);  // the new key (W1's copy)
+  const uint32_t kb0 = kq.x, kb1 = kq.y;
   const double food2 = p.start_food_random
                            ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
                            : p.start_food;
@@ -344,7 +410,7 @@ __device__ __forceinline__ void early_view_zeros(const Params& p, uint32_t e0, u
 
 // --------------------------------------------------------------------------- W0: bushes
 template <int SLOTS, int G>
-__device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+__device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const int64_t g = g0 + lane;
@@ -378,6 +444,7 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   if (lane == 0) {
     s.flag[0] = 0u;
     s.flag[1] = 0u;
+    s.flag[2] = 0u;
   }
   lds_barrier();  // B_init: the hand-off flags are clear
   int ne = (int)misc_ne(h.hdr.z), ndep = (int)misc_ndep(h.hdr.z);
@@ -502,6 +569,10 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
   count_steps(p);
   const unsigned long long jm = __ballot(job);
   if (lane == 0 && jm) p.block_resets[blockIdx.x] += (unsigned long long)__popcll(jm);
+  if (early_obs(p)) {
+    lds_await(p, &s.flag[2]);  // S rendered (W2)
+    store_units(p, s.stream, jm, false, 0, 3, lane);
+  }
   SMALL_STAMP(4);
   lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
   if (p.t_planes) {
@@ -527,14 +598,14 @@ __device__ __forceinline__ void bushes_wave(const Params& p, const SmallLayout& 
     lds_barrier();  // B3
   }
   SMALL_STAMP(5);
+  return jm;
 }
 
 // --------------------------------------------------------------------------- W1: draws
 template <int G>
-__device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+__device__ __forceinline__ unsigned long long draws_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
-  const uint32_t OB = (uint32_t)p.OB, WH = (uint32_t)p.WH;
   SMALL_STAMP(10);
   __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
   const Head h = head_load(p, g, g < p.B);
@@ -566,26 +637,6 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
   lds_barrier();  // B1
   const uint32_t info = s.info[lane];
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), s.kill[lane] != 0u);
-  // render S (:393-444) for the continuing envs (and the done ones when their terminal obs
-  // is asked for); needed only at B2, so after the reset draws W3 waits for
-  auto render = [&]() {
-  if (h.active && (!job || p.t_planes)) {
-    const uint32_t ebit = (uint32_t)lane * OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
-    M128 ost = {0ull, 0ull};
-    m_set(ost, ccb);
-    M128 wp = m_unpack(s.wolfp[lane]);
-    M128 bp = m_or(m_unpack(s.bushp[lane]), m_andn(strip_of(s, lane), m_unpack(s.gone[lane])));
-    if (p.restrict_view) {  // mask_grid (:344-357) by the fresh role
-      const M128 vm = view_mask_of(p, (int)((info >> 8) & 0xFFu));
-      wp = m_andn(wp, vm);
-      bp = m_andn(bp, vm);
-      ost = m_andn(ost, vm);
-    }
-    stream_or128(s.stream, ebit, wp);
-    stream_or128(s.stream, ebit + WH, bp);
-    stream_or128(s.stream, ebit + 2 * WH, ost);
-  }
-  };
   // the reset draws of the done envs for view cells [0, 64); W3 draws the rest and waits for
   // flag[1] before it builds the new episodes
   const unsigned long long jm = __ballot(job);
@@ -598,16 +649,24 @@ __device__ __forceinline__ void draws_wave(const Params& p, const SmallLayout& L
     reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm);
     lds_publish(&s.flag[1]);
   }
-  render();
+  if (early_obs(p)) {  // S was rendered by W2
+    lds_await(p, &s.flag[2]);
+    store_units(p, s.stream, jm, false, 1, 3, lane);
+  } else if (h.active && (!job || p.t_planes)) {
+    // S of the continuing envs (and of the done ones when their terminal obs is asked for);
+    // needed only at B2, so after the reset draws W3 waits for
+    render_s(p, s, lane, info);
+  }
   SMALL_STAMP(13);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(14);
+  return jm;
 }
 
 // --------------------------------------------------------------------------- W2: wolves
 template <int SLOTS, int G>
-__device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+__device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   const bool active = g < p.B;
@@ -701,6 +760,14 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   SMALL_STAMP(17);
   SMALL_STAMP(18);
   lds_barrier();  // B1: the spawn set, the starve flags and the bushes' counts are in
+  const uint32_t info = s.info[lane];
+  const bool starved = info_starved(info);
+  const bool job = active && p.autoreset && env_done(p, h, starved, kill);
+  const bool early = early_obs(p);
+  if (early) {  // S of the continuing envs, for the early obs stores
+    if (active && !job) render_s(p, s, lane, info);
+    lds_publish(&s.flag[2]);
+  }
 
   // spawn_wolves (:325-326): new wolves into free slots (outside the view, not in S)
   unsigned long long wolf_of = 0;
@@ -724,9 +791,6 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
   }
   // the next state of a continuing env: wolf slots and header (a done env's come from its
   // new episode)
-  const uint32_t info = s.info[lane];
-  const bool starved = info_starved(info);
-  const bool job = active && p.autoreset && env_done(p, h, starved, kill);
   if (active && !job) {
     int n = 0;
 #pragma unroll
@@ -738,15 +802,18 @@ __device__ __forceinline__ void wolves_wave(const Params& p, const SmallLayout& 
                           h.hdr.w);
   }
   if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
+  const unsigned long long jm = __ballot(job);
+  if (early) store_units(p, s.stream, jm, false, 2, 3, lane);
   SMALL_STAMP(19);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(20);
+  return jm;
 }
 
 // --------------------------------------------------------------------------- W3: ring
 template <int SLOTS, int G>
-__device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+__device__ __forceinline__ unsigned long long ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
@@ -816,6 +883,7 @@ __device__ __forceinline__ void ring_wave(const Params& p, const SmallLayout& L,
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(26);
+  return jm;
 }
 
 // --------------------------------------------------------------------------- obs stores
@@ -893,18 +961,26 @@ __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
   const SmallLayout L = small_layout(p);
   if ((int64_t)blockIdx.x * 64 >= p.B) return;  // (uniform over the workgroup)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned long long jm;  // the group's done envs (every wave computes the same mask)
+#ifdef WAB_ONLY_WAVE  // static per-wave instruction counts (tools/isa_count.py); not a runnable build
+  if (wave != WAB_ONLY_WAVE) return;
+#endif
   if (wave == 0) {
     // the bushes wave carries the longest chain and shares its SIMD with three helper waves
     // of other groups: let the arbiter issue its instructions first
     __builtin_amdgcn_s_setprio(3);
-    bushes_wave<SLOTS, G>(p, L, lds, lane);
+    jm = bushes_wave<SLOTS, G>(p, L, lds, lane);
     __builtin_amdgcn_s_setprio(0);
   }
   else if (wave == 1)
-    draws_wave<G>(p, L, lds, lane);
-  else if (wave == 2) wolves_wave<SLOTS, G>(p, L, lds, lane);
-  else ring_wave<SLOTS, G>(p, L, lds, lane);
-  if (!FEAT || p.planes) store_obs(p, lds + L.stream, threadIdx.x);
+    jm = draws_wave<G>(p, L, lds, lane);
+  else if (wave == 2) jm = wolves_wave<SLOTS, G>(p, L, lds, lane);
+  else jm = ring_wave<SLOTS, G>(p, L, lds, lane);
+  if (!FEAT && early_obs(p)) {  // the units that touch a done env (the rest went out after B1)
+    if (jm) store_units(p, lds + L.stream, jm, true, wave, 4, lane);
+  } else if (!FEAT || p.planes) {
+    store_obs(p, lds + L.stream, threadIdx.x);
+  }
   if constexpr (FEAT) step_features(p, L, lds, wave, lane);
 }
 
