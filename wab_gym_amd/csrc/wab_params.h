@@ -152,11 +152,11 @@ struct SmallLayout {
 };
 
 __host__ __device__ inline SmallLayout small_layout(const Params& p) {
+  // (the regions whose size depends on a runtime option come last, so that with the G = 11
+  // geometry every other offset is a compile-time immediate, not a live scalar register)
   SmallLayout L;
   uint32_t o = 0;
   L.tiles = o; o += lds_align4((uint32_t)p.WH);
-  L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
-  L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.stream_words = lds_align4((64u * (uint32_t)p.OB + 31u) >> 5);
   L.stream = o; o += L.stream_words + 4u;  // + slack for stream_or128's fifth dword
   L.cval = o; o += 64u;
@@ -170,6 +170,8 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.spawn = o; o += 64u * 4u;
   L.jbm = o; o += 64u * 4u;
   L.jkey = o; o += 2u * 2u * 64u;
+  L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
+  L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.fbits = L.ftab = L.fzero = L.scal = o;
   if (p.features) {  // fused features: 64 envs x F bits (+ slack), the per-cell tables (zeroed
                      // together), the envs' scalars

@@ -118,6 +118,7 @@ __device__ __forceinline__ void specialise_geometry(Params& p) {
     p.W = 11; p.H = 11; p.S = 11; p.cw = 5; p.ch = 5; p.margin = 1;
     p.OB = 363; p.WH = 121; p.R = 48; p.NT = 169; p.RW = 2; p.WHW = 4; p.SL = 11;
     p.ring_at = 124;
+    p.n_gap = 121;
     p.small_masks[0][0] = 0x00400801u; p.small_masks[0][1] = 0x00801002u;  // column 0 (j = 0)
     p.small_masks[0][2] = 0x01002004u; p.small_masks[0][3] = 0x00004008u;
     p.small_masks[1][0] = 0x00200400u; p.small_masks[1][1] = 0x00400801u;  // column H-1
@@ -259,6 +260,16 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
 }
 
 __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u; }
+
+// After B1 the new episodes (W3) are the longest chain: W3 is raised to the top issue
+// priority there and W0 lowered (A/B at B = 65536: 10.05 -> 10.02 us; -DWAB_P1_PRIO=0 off).
+// Measured and dropped: priority by workgroup age for the helper waves (+0.09 us), two or
+// four groups per workgroup (one barrier for all: 11.2 / 12.1 us), the spawn sets' gap
+// thresholds evaluated without a table (binary powering from 16 doubles in the kernel
+// arguments: 11.1 us, more SGPR spills; from device memory: 14.0 us).
+#ifndef WAB_P1_PRIO
+#define WAB_P1_PRIO 1
+#endif
 
 // the entering strip's cells are drawn in two parts, [0, kStripW1) on W1 after the tile value
 // and the rest on W3 after the spawn set (A/B: -DWAB_STRIP_W1=k)
@@ -529,6 +540,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
   SMALL_STAMP(3);
   lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
+  if constexpr (WAB_P1_PRIO) __builtin_amdgcn_s_setprio(1);
 
   // status (starve overrides kill), reward/done (:328-340), scalars, bushes and food
   const bool killed = s.kill[lane] != 0u;
@@ -858,6 +870,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   s.strip[64 + lane] = m_pack(strip_draws(p, h, b0, b1, kStripW1, 1 << 30));  // the entering strip, part 2
   SMALL_STAMP(23);
   lds_barrier();  // B1
+  if constexpr (WAB_P1_PRIO) __builtin_amdgcn_s_setprio(3);
   // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
   // (unless the terminal obs is asked for: W0 after B2) the new episodes themselves
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(s.info[lane]), s.kill[lane] != 0u);
@@ -952,15 +965,31 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
 }  // namespace
 
 // FEAT: wab_step_features (the fused featurizer); without it the feature code folds away
-template <int SLOTS, int G, bool FEAT>
-__global__ __launch_bounds__(256) void wab_step_small(Params p0) {
+// The parameter block as each wave reads it: a fresh copy from the kernel-argument segment
+// behind an opaque pointer, so that the scalar loads of its fields stay in the branch of
+// the wave that uses them.  (A plain copy of the kernel argument has every field loaded at
+// the kernel's entry, before the wave branch, and spilled to VGPR lanes: ~190 v_writelane /
+// v_readlane and a chain of scalar-load waits ahead of every wave's first global load.)
+template <int G, bool FEAT>
+__device__ __forceinline__ Params wave_params(const Params& p0) {
+#if __HIP_DEVICE_COMPILE__  // (the host pass only type-checks the kernel body)
+  typedef const Params __attribute__((address_space(4))) KernargParams;
+  KernargParams* pk = (KernargParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  Params p = *pk;
+#else
   Params p = p0;
+#endif
   specialise_geometry<G>(p);
   if constexpr (!FEAT) p.features = nullptr;
+  return p;
+}
+
+template <int SLOTS, int G, bool FEAT>
+__global__ __launch_bounds__(256) void wab_step_small(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const SmallLayout L = small_layout(p);
-  if ((int64_t)blockIdx.x * 64 >= p.B) return;  // (uniform over the workgroup)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if ((int64_t)blockIdx.x * 64 >= p0.B) return;  // (uniform over the workgroup)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (uniform branches)
   unsigned long long jm;  // the group's done envs (every wave computes the same mask)
 #ifdef WAB_ONLY_WAVE  // static per-wave instruction counts (tools/isa_count.py); not a runnable build
   if (wave != WAB_ONLY_WAVE) return;
@@ -969,13 +998,21 @@ __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
     // the bushes wave carries the longest chain and shares its SIMD with three helper waves
     // of other groups: let the arbiter issue its instructions first
     __builtin_amdgcn_s_setprio(3);
-    jm = bushes_wave<SLOTS, G>(p, L, lds, lane);
+    const Params p = wave_params<G, FEAT>(p0);
+    jm = bushes_wave<SLOTS, G>(p, small_layout(p), lds, lane);
     __builtin_amdgcn_s_setprio(0);
+  } else if (wave == 1) {
+    const Params p = wave_params<G, FEAT>(p0);
+    jm = draws_wave<G>(p, small_layout(p), lds, lane);
+  } else if (wave == 2) {
+    const Params p = wave_params<G, FEAT>(p0);
+    jm = wolves_wave<SLOTS, G>(p, small_layout(p), lds, lane);
+  } else {
+    const Params p = wave_params<G, FEAT>(p0);
+    jm = ring_wave<SLOTS, G>(p, small_layout(p), lds, lane);
   }
-  else if (wave == 1)
-    jm = draws_wave<G>(p, L, lds, lane);
-  else if (wave == 2) jm = wolves_wave<SLOTS, G>(p, L, lds, lane);
-  else jm = ring_wave<SLOTS, G>(p, L, lds, lane);
+  const Params p = wave_params<G, FEAT>(p0);
+  const SmallLayout L = small_layout(p);
   if (!FEAT && early_obs(p)) {  // the units that touch a done env (the rest went out after B1)
     if (jm) store_units(p, lds + L.stream, jm, true, wave, 4, lane);
   } else if (!FEAT || p.planes) {
