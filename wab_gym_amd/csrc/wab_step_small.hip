@@ -74,16 +74,45 @@ struct Head {
   uint64_t kenv;
 };
 
-__device__ __forceinline__ Head head_load(const Params& p, int64_t g, bool active) {
+// The header and action loads (head_fetch) are issued together with the rest of a wave's
+// loads, and decoded (head_decode) only after all of them are in flight: a use between two
+// groups of loads makes the second group wait a full memory round trip for the first.
+struct HeadRaw {
+  uint4 hdr;
+  int a;
+};
+// (loads are unconditional, from env 0 for an inactive lane, so that no branch splits a
+// wave's loads; head_decode zeroes an inactive lane's header)
+__device__ __forceinline__ HeadRaw head_fetch(const Params& p, int64_t g, bool active) {
+  const int64_t gl = active ? g : 0;
+  HeadRaw r;
+  r.hdr = p.hdr[gl];
+  r.a = (int)p.actions[gl];
+  return r;
+}
+
+// An opaque copy: whatever uses the value comes after this point.  Placed after a wave's last
+// load, it keeps the compiler from folding the first uses of each loaded value (a +1, a
+// mask) into the load's own block, where the wait for that load would stall the loads after
+// it (one s_waitcnt for all of them instead of one per group).
+template <typename T>
+__device__ __forceinline__ void opaque(T& v) {
+  asm volatile("" : "+v"(v));
+}
+__device__ __forceinline__ void opaque(HeadRaw& r) {
+  opaque(r.hdr.x);
+  opaque(r.hdr.y);
+  opaque(r.hdr.z);
+  opaque(r.hdr.w);
+  opaque(r.a);
+}
+
+__device__ __forceinline__ Head head_decode(const Params& p, int64_t g, bool active, const HeadRaw& r) {
   Head h;
   h.active = active;
-  h.hdr = make_uint4(0u, 0u, 0u, 0u);
-  int a = 0;
-  if (active) {
-    h.hdr = p.hdr[g];
-    a = (int)p.actions[g];
-  }
-  h.kenv = env_key(p.seed, (uint64_t)(p.env_base + g));  // overlaps the loads
+  h.hdr = active ? r.hdr : make_uint4(0u, 0u, 0u, 0u);
+  const int a = active ? r.a : 0;
+  h.kenv = env_key(p.seed, (uint64_t)(p.env_base + g));
   h.ox = xy_x(h.hdr.x);
   h.oy = xy_y(h.hdr.x);
   h.turn = (int32_t)h.hdr.y + 1;
@@ -434,24 +463,42 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   double food = 0.0;
   uint32_t bw0 = 0u, bw1 = 0u, bw2 = 0u, bw3 = 0u;
   uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
-  const Head h = head_load(p, g, active);
-  if (active) {
-    food = p.food[g];
-    bw0 = p.bushmap[g];
-    if (p.WHW > 1) bw1 = p.bushmap[p.B + g];
-    if (p.WHW > 2) bw2 = p.bushmap[2 * p.B + g];
-    if (p.WHW > 3) bw3 = p.bushmap[3 * p.B + g];
+  HeadRaw hr = head_fetch(p, g, active);
+  {  // (unconditional: an inactive lane reads env 0; entries at or past eaten_cap read the
+     // last entry and are never used, entry i counts only below the log length <= cap)
+    const int64_t gl = active ? g : 0;
+    food = p.food[gl];
+    bw0 = p.bushmap[gl];
+    if (p.WHW > 1) bw1 = p.bushmap[p.B + gl];
+    if (p.WHW > 2) bw2 = p.bushmap[2 * p.B + gl];
+    if (p.WHW > 3) bw3 = p.bushmap[3 * p.B + gl];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < p.eaten_cap) {
-        lxy[i] = p.eaten_xy[(int64_t)i * p.B + g];
-        lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int64_t at = (int64_t)min(i, p.eaten_cap - 1) * p.B + gl;
+      lxy[i] = p.eaten_xy[at];
+      lrem[i] = p.eaten_rem[at];
+    }
+  }
+  opaque(hr);
+  opaque(food);
+  opaque(bw0);
+  opaque(bw1);
+  opaque(bw2);
+  opaque(bw3);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    opaque(lxy[i]);
+    opaque(lrem[i]);
+  }
+  if (!active) {  // (env 0's values: an inactive lane must not eat, log or store anything)
+    food = 0.0;
+    bw0 = bw1 = bw2 = bw3 = 0u;
   }
   {
     uint4* z = reinterpret_cast<uint4*>(s.stream);
     for (uint32_t i = lane; i < L.stream_words / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  const Head h = head_decode(p, g, active, hr);
   if (lane == 0) {
     s.flag[0] = 0u;
     s.flag[1] = 0u;
@@ -620,17 +667,21 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(10);
   __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
-  const Head h = head_load(p, g, g < p.B);
+  HeadRaw hr = head_fetch(p, g, g < p.B);
   {  // every threshold load in flight at once (a copy loop waits for each before the next)
     const int nthr = p.max_berries;  // <= 255
     uint64_t tv[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
+    for (int k = 0; k < 4; ++k) tv[k] = p.thresholds[min(64 * k + lane, max(nthr, 1) - 1)];  // (>= 1 entry)
+    opaque(hr);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) opaque(tv[k]);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (64 * k + lane < nthr) s.thr[64 * k + lane] = tv[k];
     if (lane == 0) bush_thr_pads(s.thr, nthr);
   }
+  const Head h = head_decode(p, g, g < p.B, hr);
   lds_barrier();  // B_init
   SMALL_STAMP(30);
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
@@ -690,11 +741,16 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   uint32_t wr[SLOTS];
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
-  if (active) {
+  {
+    const int64_t gl = active ? g : 0;  // (unconditional; an inactive lane has no live wolf)
 #pragma unroll
-    for (int k = 0; k < kSpecSlots; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
+    for (int k = 0; k < kSpecSlots; ++k) wr[k] = p.wolves[(int64_t)k * p.B + gl];  // speculatively
   }
-  const Head h = head_load(p, g, active);
+  HeadRaw hr = head_fetch(p, g, active);
+  opaque(hr);
+#pragma unroll
+  for (int k = 0; k < kSpecSlots; ++k) opaque(wr[k]);
+  const Head h = head_decode(p, g, active, hr);
   lds_barrier();  // B_init
   SMALL_STAMP(28);
   const int nw = (int)misc_nw(h.hdr.z);
@@ -829,7 +885,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
-  const Head h = head_load(p, g, g < p.B);
+  HeadRaw hr = head_fetch(p, g, g < p.B);
   if constexpr (G == 11) {  // view-cell offsets (cw - i, ch - j) of cell c = 11 i + j, computed
     for (int c = lane; c < 121; c += 64) s.tiles[c] = xy_pack(5 - c / 11, 5 - c % 11);
   } else {
@@ -846,6 +902,9 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
     uint64_t gv[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) gv[k] = p.gap[min(64 * k + lane, n - 1)];
+    opaque(hr);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) opaque(gv[k]);
 #pragma unroll
     for (int k = 0; k < 3; ++k)
       if (64 * k + lane < n) s.gap[64 * k + lane] = gv[k];
@@ -854,6 +913,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
     uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
     for (uint32_t i = lane; i < L.fzero / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  const Head h = head_decode(p, g, g < p.B, hr);
   lds_barrier();  // B_init
   if (p.features) {
     feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
