@@ -133,9 +133,9 @@ bool small_map(const Params& p) { return p.WHW <= 4; }
 enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1, KERNEL_WIDE = 2 };
 
 // (W, H >= 3: the strip that scrolls into view, drawn on another wave, never holds the
-// ostrich's tile)
+// ostrich's tile; W, H <= 32: its bits are one dword)
 bool small_view(const Params& p) {
-  return p.WH <= 128 && p.W >= 3 && p.H >= 3 && p.S == p.H && p.R <= 128 &&
+  return p.WH <= 128 && p.W >= 3 && p.H >= 3 && p.W <= 32 && p.H <= 32 && p.S == p.H && p.R <= 128 &&
          (!p.restrict_view || (p.W == 11 && p.H == 11));
 }
 

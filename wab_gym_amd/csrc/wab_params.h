@@ -164,7 +164,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.wolfp = o; o += 64u * 4u;
   L.kill = o; o += 64u;
   L.bushp = o; o += 64u * 4u;
-  L.strip = o; o += 2u * 64u * 4u;
+  L.strip = o; o += 2u * 64u;
   L.gone = o; o += 64u * 4u;
   L.info = o; o += 64u;
   L.spawn = o; o += 64u * 4u;

@@ -206,22 +206,25 @@ __device__ __forceinline__ void reset_chunk(const Params& p, const uint32_t* til
   if (n_jobs - j == 1) reset_draws<1>(p, jkey, j, xy, c, jbm);
 }
 
-// the row or column that scrolled into view (generate_bushes :613-629): the bush bits of its
-// cells [c0, c1) (multiples of 4)
-__device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint32_t b0, uint32_t b1, int c0, int c1) {
-  M128 nb = {0ull, 0ull};
+// the row or column that scrolled into view (generate_bushes :613-629): bit k is the bush
+// presence of its cell k (x moves: row i0, cell (i0, k); y moves: column j0, cell (k, j0)),
+// for the cells [c0, c1) (multiples of 4).  Consecutive cells are one tile apart, so their
+// packed tiles are one packed 16-bit add from the first.
+__device__ __forceinline__ uint32_t strip_draws(const Params& p, const Head& h, uint32_t b0, uint32_t b1, int c0,
+                                                int c1) {
+  uint32_t hits = 0;
   if (h.dir != DIR_STAY) {
     const bool horiz = h.dir == DIR_RIGHT || h.dir == DIR_LEFT;
     const int n = horiz ? p.H : p.W;
     const int i0 = h.dir == DIR_LEFT ? p.W - 1 : 0, j0 = h.dir == DIR_DOWN ? p.H - 1 : 0;
+    const uint32_t xy0 = horiz ? xy_pack(h.ox - (i0 - p.cw), h.oy + p.ch) : xy_pack(h.ox + p.cw, h.oy - (j0 - p.ch));
     const uint32_t ts = make_ts(SITE_BUSH, 0, 0), hk = ts ^ b1;
     for (int c = c0; c < min(c1, p.SL); c += 4) {
-      uint32_t h1[4], hh[4], cb[4];
+      uint32_t h1[4], hh[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int i = horiz ? i0 : c + k, j = horiz ? c + k : j0;
-        cb[k] = (uint32_t)(i * p.H + j);
-        h1[k] = xy_pack(h.ox - (i - p.cw), h.oy - (j - p.ch)) ^ b0;
+      for (int k = 0; k < 4; ++k) {  // cell c + k: the first tile minus c + k in y (x moves) or x
+        const uint32_t d = (uint32_t)(-(c + k)) & 0xFFFFu;
+        h1[k] = xy_add(xy0, horiz ? d << 16 : d) ^ b0;
       }
       fmix32x4(h1);
 #pragma unroll
@@ -233,18 +236,31 @@ __device__ __forceinline__ M128 strip_draws(const Params& p, const Head& h, uint
         hit |= (hh[k] > p.bush_th ? 1u : 0u) << k;
         tie |= (hh[k] == p.bush_th ? 1u : 0u) << k;
       }
-      const uint32_t in = n - c >= 4 ? 0xFu : (n > c ? (1u << (n - c)) - 1u : 0u);
-      if (tie & in) {
+      if (tie) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (((tie >> k) & 1u) && draw_lo21(h1[k], ts, b0) >= p.bush_tl) hit |= 1u << k;
       }
-      hit &= in;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) set_bit_if(nb, cb[k], (hit >> k) & 1u);
+      hits |= hit << c;
     }
+    hits &= n >= 32 ? ~0u : (1u << n) - 1u;
   }
-  return nb;
+  return hits;
+}
+
+// the strip's bits (strip_draws) as view cells: row i0 is the bits [i0 H, i0 H + H), column
+// j0 the bits k H + j0
+__device__ __forceinline__ M128 strip_cells(const Params& p, int dir, uint32_t hits) {
+  M128 m = {0ull, 0ull};
+  if (!hits) return m;
+  if (dir == DIR_RIGHT || dir == DIR_LEFT) {
+    m.lo = hits;
+    shl128(m.lo, m.hi, dir == DIR_LEFT ? (p.W - 1) * p.H : 0);
+  } else {
+    const uint32_t j0 = dir == DIR_DOWN ? (uint32_t)p.H - 1u : 0u;
+    for (uint32_t b = hits; b; b &= b - 1u) m_set(m, (uint32_t)(__ffs(b) - 1) * (uint32_t)p.H + j0);
+  }
+  return m;
 }
 
 struct Lds {
@@ -258,7 +274,7 @@ struct Lds {
   uint4* wolfp;     // [64] wolf grid of S (W2, P0)
   uint32_t* kill;   // [64] (W2, P0)
   uint4* bushp;     // [64] bush grid of S without the entering strip (W0, P0)
-  uint4* strip;     // [2][64] bush bits of the strip that scrolled into view (W1, W3; P0)
+  uint32_t* strip;  // [2][64] bush bits of the strip that scrolled into view (W1, W3; P0)
   uint4* gone;      // [64] emptied tiles in view (W0, P0): cleared from the strip too
   uint32_t* info;   // [64] starved | role << 8 | eaten << 16 | emptied << 24 (W0, P0)
   uint4* spawn;     // [64] ring spawn sets (W3)
@@ -278,7 +294,7 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   s.wolfp = reinterpret_cast<uint4*>(lds + L.wolfp);
   s.kill = lds + L.kill;
   s.bushp = reinterpret_cast<uint4*>(lds + L.bushp);
-  s.strip = reinterpret_cast<uint4*>(lds + L.strip);
+  s.strip = lds + L.strip;
   s.gone = reinterpret_cast<uint4*>(lds + L.gone);
   s.info = lds + L.info;
   s.spawn = reinterpret_cast<uint4*>(lds + L.spawn);
@@ -306,8 +322,8 @@ __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u
 #define WAB_STRIP_W1 8
 #endif
 constexpr int kStripW1 = WAB_STRIP_W1;
-__device__ __forceinline__ M128 strip_of(const Lds& s, int lane) {
-  return m_or(m_unpack(s.strip[lane]), m_unpack(s.strip[64 + lane]));
+__device__ __forceinline__ M128 strip_of(const Params& p, const Lds& s, int lane, int dir) {
+  return strip_cells(p, dir, s.strip[lane] | s.strip[64 + lane]);
 }
 
 // scan eaten-log entries [i0, i0 + 4): the entry on the ostrich's tile, and the emptied
@@ -331,13 +347,13 @@ __device__ __forceinline__ void scan_log(const Params& p, const Head& h, const u
 // render S (:393-444) of one env into the bit-stream: the wolf grid (W2), the bush grid (W0,
 // plus the entering strip, W1/W3, minus emptied tiles), the ostrich; mask_grid (:344-357) by
 // the fresh role
-__device__ __forceinline__ void render_s(const Params& p, const Lds& s, int lane, uint32_t info) {
+__device__ __forceinline__ void render_s(const Params& p, const Lds& s, int lane, uint32_t info, int dir) {
   const uint32_t WH = (uint32_t)p.WH;
   const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
   M128 ost = {0ull, 0ull};
   m_set(ost, ccb);
   M128 wp = m_unpack(s.wolfp[lane]);
-  M128 bp = m_or(m_unpack(s.bushp[lane]), m_andn(strip_of(s, lane), m_unpack(s.gone[lane])));
+  M128 bp = m_or(m_unpack(s.bushp[lane]), m_andn(strip_of(p, s, lane, dir), m_unpack(s.gone[lane])));
   if (p.restrict_view) {
     const M128 vm = view_mask_of(p, (int)((info >> 8) & 0xFFu));
     wp = m_andn(wp, vm);
@@ -615,7 +631,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     }
     if (p.features && !job) s.scal[lane] = (uint32_t)ft | ((uint32_t)role << 8) | ((uint32_t)status << 16);
     if (!job) {
-      bm = m_or(bm, m_andn(strip_of(s, lane), gone));
+      bm = m_or(bm, m_andn(strip_of(p, s, lane, h.dir), gone));
       p.bushmap[g] = m_word<0>(bm);
       if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(bm);
       if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(bm);
@@ -695,7 +711,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   if (p.features && !p.restrict_view)  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
   SMALL_STAMP(11);
-  s.strip[lane] = m_pack(strip_draws(p, h, b0, b1, 0, kStripW1));  // generate_bushes (:613-629): the entering strip
+  s.strip[lane] = strip_draws(p, h, b0, b1, 0, kStripW1);  // generate_bushes (:613-629): the entering strip
   SMALL_STAMP(12);
   lds_barrier();  // B1
   const uint32_t info = s.info[lane];
@@ -718,7 +734,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   } else if (h.active && (!job || p.t_planes)) {
     // S of the continuing envs (and of the done ones when their terminal obs is asked for);
     // needed only at B2, so after the reset draws W3 waits for
-    render_s(p, s, lane, info);
+    render_s(p, s, lane, info, h.dir);
   }
   SMALL_STAMP(13);
   lds_barrier();  // B2
@@ -833,7 +849,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   const bool job = active && p.autoreset && env_done(p, h, starved, kill);
   const bool early = early_obs(p);
   if (early) {  // S of the continuing envs, for the early obs stores
-    if (active && !job) render_s(p, s, lane, info);
+    if (active && !job) render_s(p, s, lane, info, h.dir);
     lds_publish(&s.flag[2]);
   }
 
@@ -927,7 +943,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   if (p.wolves_on && h.active)
     spawn_hits(s.gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, b0, b1, [&](int r) { m_set(spawn, (uint32_t)r); });
   s.spawn[lane] = m_pack(spawn);
-  s.strip[64 + lane] = m_pack(strip_draws(p, h, b0, b1, kStripW1, 1 << 30));  // the entering strip, part 2
+  s.strip[64 + lane] = strip_draws(p, h, b0, b1, kStripW1, 1 << 30);  // the entering strip, part 2
   SMALL_STAMP(23);
   lds_barrier();  // B1
   if constexpr (WAB_P1_PRIO) __builtin_amdgcn_s_setprio(3);
