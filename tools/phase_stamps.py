@@ -171,10 +171,13 @@ def small_report(env, st, g, steps):
     acc = {k: [] for k in waves}
     spans, ends = [], []
     by_xcd, slow_w0, fast_w0, start_off = [], [], [], []
-    # extra stamps: W2 28 after B_init, 29 after despawn; W1 30 after B_init, 31 after the key
+    # extra stamps: W2 28 after B_init, 29 after despawn; W1 30 after B_init, 31 after the key;
+    # W3 24 after its reset draws, 9 after the wait for W1's (groups without a done env
+    # leave 24 and 9 at 0: only groups with one are averaged)
     DETAIL = {"W2 start->B_init": (16, 28), "W2 B_init->despawned": (28, 29), "W2 despawned->grid": (29, 17),
               "W1 start->B_init": (10, 30), "W1 key": (30, 31), "W1 tile value": (31, 11),
-              "W0 start->W2 B_init": (0, 28)}
+              "W0 start->W2 B_init": (0, 28),
+              "W3 B1 + reset draws": (23, 24), "W3 await W1": (24, 9), "W3 new episodes": (9, 25)}
     detail = []
     for t in range(steps):
         st.zero_()
@@ -197,7 +200,11 @@ def small_report(env, st, g, steps):
         slow_w0.append(d0[order[-len(order) // 20:]].mean(axis=0))
         fast_w0.append(d0[order[: len(order) // 4]].mean(axis=0))
         start_off.append(((s[:, 0] - t0)[order[-len(order) // 20:]].mean(), (s[:, 0] - t0)[order[: len(order) // 4]].mean()))
-        detail.append([(s[:, a1] - s[:, a0]).mean() for a0, a1 in DETAIL.values()])
+        row = []
+        for a0, a1 in DETAIL.values():
+            ok = (s[:, a0] > 0) & (s[:, a1] > 0)
+            row.append((s[ok, a1] - s[ok, a0]).mean() if ok.any() else 0.0)
+        detail.append(row)
     for k, (cols, names) in waves.items():
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s:" % k)

@@ -344,25 +344,32 @@ __device__ __forceinline__ void scan_log(const Params& p, const Head& h, const u
   }
 }
 
+// the ostrich's own cell of an obs segment: one bit (mask_grid never blinds the centre, but
+// the mask is applied all the same)
+__device__ __forceinline__ void stream_set_ostrich(const Params& p, uint32_t* stream, uint32_t ebit, int role) {
+  const uint32_t ccb = (uint32_t)(p.cw * p.H + p.ch);
+  if (p.restrict_view && m_test(view_mask_of(p, role), ccb)) return;
+  const uint32_t bit = ebit + 2u * (uint32_t)p.WH + ccb;
+  atomicOr(&stream[bit >> 5], 1u << (bit & 31u));
+}
+
 // render S (:393-444) of one env into the bit-stream: the wolf grid (W2), the bush grid (W0,
 // plus the entering strip, W1/W3, minus emptied tiles), the ostrich; mask_grid (:344-357) by
 // the fresh role
 __device__ __forceinline__ void render_s(const Params& p, const Lds& s, int lane, uint32_t info, int dir) {
   const uint32_t WH = (uint32_t)p.WH;
-  const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, ccb = (uint32_t)(p.cw * p.H + p.ch);
-  M128 ost = {0ull, 0ull};
-  m_set(ost, ccb);
+  const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB;
+  const int role = (int)((info >> 8) & 0xFFu);
   M128 wp = m_unpack(s.wolfp[lane]);
   M128 bp = m_or(m_unpack(s.bushp[lane]), m_andn(strip_of(p, s, lane, dir), m_unpack(s.gone[lane])));
   if (p.restrict_view) {
-    const M128 vm = view_mask_of(p, (int)((info >> 8) & 0xFFu));
+    const M128 vm = view_mask_of(p, role);
     wp = m_andn(wp, vm);
     bp = m_andn(bp, vm);
-    ost = m_andn(ost, vm);
   }
-  stream_or128(s.stream, ebit, wp);
+  if (wp.lo | wp.hi) stream_or128(s.stream, ebit, wp);  // (most envs see no wolf)
   stream_or128(s.stream, ebit + WH, bp);
-  stream_or128(s.stream, ebit + 2 * WH, ost);
+  stream_set_ostrich(p, s.stream, ebit, role);
 }
 
 // Early obs stores (plain steps of full groups: no terminal obs, no fused features): the
@@ -403,33 +410,27 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
 // The new episode of a done env (reset :231-248, spawn_ostriches :595-611): state, scalars,
 // initial wolves (initialize_wolves :578-593: the view's spawn set at turn 0), and its obs
 // segment (which must be clear) from the job's reset draws.
+// The new episode of a done env (reset :231-248, spawn_ostriches :595-611) in two parts: A
+// needs only the new key (state, scalars, initial wolves = the view's spawn set at turn 0,
+// initialize_wolves :578-593, and the wolf and ostrich planes of its obs segment, which must
+// be clear); B the job's reset bush draws (bushmap, bush plane).  Returns the new role.
 template <int SLOTS>
-__device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const Head& h, int64_t g, int j,
-                                            uint32_t ebit, unsigned long long& wolf_of) {
-  const uint32_t WH = (uint32_t)p.WH, ccb = (uint32_t)(p.cw * p.H + p.ch);
-  const uint2 kq = *reinterpret_cast<const uint2*>(&s.jkey[2 * j]);  // the new key (W1's copy)
-  const uint32_t kb0 = kq.x, kb1 = kq.y;
+__device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, const Head& h, int64_t g, uint32_t kb0,
+                                             uint32_t kb1, uint32_t ebit, unsigned long long& wolf_of) {
   const double food2 = p.start_food_random
                            ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
                            : p.start_food;
   const int role2 = p.start_role_random
                         ? (int)(draw_U(xy_pack(0, 0), make_ts(SITE_START_ROLE, 0, 0), kb0, kb1) >> 52)
                         : p.start_role;
-  const M128 nbm = m_unpack(*reinterpret_cast<const uint4*>(&s.jbm[4 * j]));
   M128 nwm = {0ull, 0ull};
   if (p.wolves_on)
     spawn_hits(s.gap, p.WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, kb0, kb1, [&](int c) { m_set(nwm, (uint32_t)c); });
-  M128 ost = {0ull, 0ull}, wp = nwm, bp = nbm;
-  m_set(ost, ccb);
-  if (p.restrict_view) {
-    const M128 vm = view_mask_of(p, role2);
-    wp = m_andn(wp, vm);
-    bp = m_andn(bp, vm);
-    ost = m_andn(ost, vm);
+  if (nwm.lo | nwm.hi) {
+    const M128 wp = p.restrict_view ? m_andn(nwm, view_mask_of(p, role2)) : nwm;
+    stream_or128(s.stream, ebit, wp);
   }
-  stream_or128(s.stream, ebit, wp);
-  stream_or128(s.stream, ebit + WH, bp);
-  stream_or128(s.stream, ebit + 2 * WH, ost);
+  stream_set_ostrich(p, s.stream, ebit, role2);
   int n = 0;  // initial wolves, one per wolf cell of the view (slot order is irrelevant)
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -441,10 +442,6 @@ __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const
       else wolf_of += 1;
     }
   }
-  p.bushmap[g] = m_word<0>(nbm);
-  if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(nbm);
-  if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(nbm);
-  if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(nbm);
   p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
   p.food[g] = food2;
   const uint32_t ft2 = (uint32_t)(int)ceil(food2 * (double)p.turns_empty);
@@ -452,6 +449,17 @@ __device__ __forceinline__ void new_episode(const Params& p, const Lds& s, const
   p.role[g] = (uint8_t)role2;
   p.status[g] = 0;
   if (p.features) s.scal[(int)(g & 63)] = ft2 | ((uint32_t)role2 << 8);
+  return role2;
+}
+
+__device__ __forceinline__ void new_episode_b(const Params& p, const Lds& s, int64_t g, int j, uint32_t ebit,
+                                              int role2) {
+  const M128 nbm = m_unpack(*reinterpret_cast<const uint4*>(&s.jbm[4 * j]));
+  stream_or128(s.stream, ebit + (uint32_t)p.WH, p.restrict_view ? m_andn(nbm, view_mask_of(p, role2)) : nbm);
+  p.bushmap[g] = m_word<0>(nbm);
+  if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(nbm);
+  if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(nbm);
+  if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(nbm);
 }
 
 // --------------------------------------------------------------------------- fused features: early lines
@@ -666,7 +674,10 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
       if (job) {
         const uint32_t ebit = (uint32_t)lane * OB;
         stream_clear(s.stream, ebit, OB);
-        new_episode<SLOTS>(p, s, h, g, __popcll(jm & ((1ull << lane) - 1ull)), ebit, wolf_of);
+        const int j = __popcll(jm & ((1ull << lane) - 1ull));
+        const uint2 kq = *reinterpret_cast<const uint2*>(&s.jkey[2 * j]);  // the new key (W1's copy)
+        const int role2 = new_episode_a<SLOTS>(p, s, h, g, kq.x, kq.y, ebit, wolf_of);
+        new_episode_b(p, s, g, j, ebit, role2);
       }
     }
     if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
@@ -954,17 +965,24 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   if (jm) {
     const int j = __popcll(jm & ((1ull << lane) - 1ull));
     uint32_t* jkey = s.jkey + 2 * 64;  // this wave's copy of the keys
+    uint64_t ek2 = 0;
     if (job) {
-      const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
+      ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
       *reinterpret_cast<uint2*>(&jkey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
     }
     const int n_jobs = __popcll(jm);
     for (uint32_t c0 = 64; c0 < (uint32_t)p.WH; c0 += 64)  // cells [0, 64): W1
       reset_chunk(p, s.tiles, jkey, n_jobs, c0, lane, s.jbm);
+    SMALL_STAMP(24);
     if (!p.t_planes) {
-      lds_await(p, &s.flag[1]);  // W1's part of the draws
+      // the part of the new episode that needs only its key, while W1 may still be drawing
       unsigned long long wolf_of = 0;
-      if (job) new_episode<SLOTS>(p, s, h, g, j, (uint32_t)lane * (uint32_t)p.OB, wolf_of);
+      const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB;
+      int role2 = 0;
+      if (job) role2 = new_episode_a<SLOTS>(p, s, h, g, (uint32_t)ek2, (uint32_t)(ek2 >> 32), ebit, wolf_of);
+      lds_await(p, &s.flag[1]);  // W1's part of the draws
+      SMALL_STAMP(9);
+      if (job) new_episode_b(p, s, g, j, ebit, role2);
       if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     }
   }
