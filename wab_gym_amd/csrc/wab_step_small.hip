@@ -306,6 +306,8 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
 
 __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u; }
 
+// (Measured and reverted: the key-only part of the new episodes on W0 after its own P1 work
+// instead of on W3 before its wait for W1: 9.05 -> 9.57 us.)
 // After B1 the new episodes (W3) are the longest chain: W3 is raised to the top issue
 // priority there and W0 lowered (A/B at B = 65536: 10.05 -> 10.02 us; -DWAB_P1_PRIO=0 off).
 // Measured and dropped: priority by workgroup age for the helper waves (+0.09 us), two or
