@@ -29,7 +29,8 @@ Bernoulli(q) over the tiles.  The same joint law is drawn here by geometric gaps
 canonical tile order (the ring order `ring_index`, or the view-cell order `view_index`
 for `initialize_wolves`): the number of misses before the next hit among the m tiles left
 is G = #{g in 1..m : U_k < P[g]}, P[g] = floor((1 - q)^g * 2^53) (`gap_thresholds`), with
-U_k the site-6 draw of the k-th gap; G = m ends the set (`spawn_hits`).  A step with no
+U_k the site-6 draw of the k-th gap; G = m ends the set (`spawn_hits`; the tiles are
+taken in chunks of 128, each its own sequence, so that P is a 129-entry table).  A step with no
 spawn (~97.6 % at the defaults) costs ONE draw instead of one per ring tile.  The
 per-tile uniforms the reference sees are then drawn conditionally on the set
 (`conditional_spawn_U`: below q on a hit tile, at or above q elsewhere, each from the
@@ -164,18 +165,28 @@ def gap_count(U: int, P: list, m: int) -> int:
     return lo
 
 
+GAP_CHUNK = 128  # tiles per gap sequence: P is needed for g <= 128 only (a small table)
+
+
 def spawn_hits(ek: int, turn: int, n: int, P: list) -> list:
-    """Ascending indices in [0, n) of the tiles that spawn a wolf at `turn` (iid Bernoulli(q))."""
-    hits, pos, k = [], 0, 0
-    while pos < n:
-        U = int(draw_U(ek, SITE_GAP, turn, [k & 0xFFFF], [k >> 16], 0)[0])
-        G = gap_count(U, P, n - pos)
-        if G >= n - pos:
-            break
-        pos += G
-        hits.append(pos)
-        pos += 1
-        k += 1
+    """Ascending indices in [0, n) of the tiles that spawn a wolf at `turn` (iid Bernoulli(q)).
+
+    The tiles are taken in chunks of GAP_CHUNK, each its own gap sequence: the k-th draw of
+    chunk c is the site-6 draw of "tile" (k, c).  P = gap_thresholds(T, >= GAP_CHUNK)."""
+    hits = []
+    for c in range((n + GAP_CHUNK - 1) // GAP_CHUNK):
+        base = c * GAP_CHUNK
+        m = min(GAP_CHUNK, n - base)
+        pos, k = 0, 0
+        while pos < m:
+            U = int(draw_U(ek, SITE_GAP, turn, [k], [c], 0)[0])
+            G = gap_count(U, P, m - pos)
+            if G >= m - pos:
+                break
+            pos += G
+            hits.append(base + pos)
+            pos += 1
+            k += 1
     return hits
 
 

@@ -75,16 +75,21 @@ static int gap_count(uint64_t U, const uint64_t* P, int m) {
   return lo;
 }
 
-/* calls hit(ctx, index) for each tile in [0, n) that spawns a wolf at `turn`, ascending */
+/* calls hit(ctx, index) for each tile in [0, n) that spawns a wolf at `turn`, ascending;
+ * chunks of 128 tiles, each its own gap sequence (draw k of chunk c: "tile" (k, c)) */
+enum { GAP_CHUNK = 128 };
 static void spawn_hits(uint64_t ek, int64_t turn, int n, const uint64_t* P, void (*hit)(void*, int), void* ctx) {
-  int pos = 0;
-  for (uint32_t k = 0; pos < n; ++k) {
-    const uint64_t U = wabo_draw_U(ek, SITE_GAP, turn, (int64_t)(k & 0xFFFFu), (int64_t)(k >> 16), 0);
-    const int G = gap_count(U, P, n - pos);
-    if (G >= n - pos) break;
-    pos += G;
-    hit(ctx, pos);
-    pos += 1;
+  for (int c = 0; c * GAP_CHUNK < n; ++c) {
+    const int base = c * GAP_CHUNK, m = n - base < GAP_CHUNK ? n - base : GAP_CHUNK;
+    int pos = 0;
+    for (uint32_t k = 0; pos < m; ++k) {
+      const uint64_t U = wabo_draw_U(ek, SITE_GAP, turn, (int64_t)k, (int64_t)c, 0);
+      const int G = gap_count(U, P, m - pos);
+      if (G >= m - pos) break;
+      pos += G;
+      hit(ctx, base + pos);
+      pos += 1;
+    }
   }
 }
 
@@ -117,7 +122,7 @@ struct wabo_batch {
   int n_actions;
   int act_dx[6], act_dy[6], act_role[6]; /* act_role -1 = NaN (no role change) */
   uint64_t keep_gt, spawn_lt;
-  uint64_t* gap; /* gap_thresholds(spawn_lt, max(ring, view)) */
+  uint64_t* gap; /* gap_thresholds(spawn_lt, GAP_CHUNK) */
   double fill, hunger;
   int stride, plane_bytes, obs_bytes;
   oenv* envs;
@@ -265,11 +270,7 @@ wabo_batch* wabo_create(const wab_config* cfg, int64_t batch, uint64_t seed, int
   /* u > despawn keeps a wolf (:263); u < chance/2 spawns one (:573) */
   b->keep_gt = (uint64_t)floor(ldexp(cfg->wolf_chance_to_despawn, 53));
   b->spawn_lt = (uint64_t)ceil(ldexp(cfg->chance_wolf_on_square / 2.0, 53));
-  {
-    const int m = cfg->wolf_spawn_margin, WH = cfg->width * cfg->height;
-    const int R = (cfg->width + 2 * m) * (cfg->height + 2 * m) - WH;
-    b->gap = gap_thresholds(b->spawn_lt, R > WH ? R : WH);
-  }
+  b->gap = gap_thresholds(b->spawn_lt, GAP_CHUNK);
   b->fill = 1.0 / (double)cfg->turns_to_fill_food;    /* :307-309 */
   b->hunger = 1.0 / (double)cfg->turns_to_empty_food; /* :316 */
   b->stride = cfg->plane_stride > 0 ? cfg->plane_stride : cfg->height;

@@ -151,7 +151,7 @@ def _spawn_draws(env, ek, fn, new_wolves):
         n = (W + 2 * m) * (H + 2 * m) - W * H
     if sorted(idx) != list(range(n)):
         raise RuntimeError("keyed RNG: %s tiles are not the %d-tile canonical set" % (fn, n))
-    hits = set(kr.spawn_hits(ek, turn, n, kr.gap_thresholds(T, n)))
+    hits = set(kr.spawn_hits(ek, turn, n, kr.gap_thresholds(T, kr.GAP_CHUNK)))
     V = kr.draw_U(ek, kr.SITE_SPAWN, turn, xs, ys, 0)
     U = [kr.conditional_spawn_U(int(v), T, i in hits) for v, i in zip(V.tolist(), idx)]
     return np.asarray(U, dtype=np.float64) * 2.0 ** -53

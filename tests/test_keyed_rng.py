@@ -58,7 +58,7 @@ def test_gap_thresholds_match_c():
     for chance, margin in ((0.001, 1), (0.02, 1), (0.06, 2), (0.0, 1), (1.0, 1)):
         b = _batch(chance, wolf_spawn_margin=margin)
         T = kr.hit_threshold_lt(chance / 2)
-        n = max((11 + 2 * margin) ** 2 - 121, 121)
+        n = kr.GAP_CHUNK  # the oracle table (spawn sets are drawn in chunks of GAP_CHUNK tiles)
         P = kr.gap_thresholds(T, n)
         assert P[0] == 2**53 and all(P[g] >= P[g + 1] for g in range(n))
         for g in range(n + 1):
@@ -68,11 +68,11 @@ def test_gap_thresholds_match_c():
 def test_spawn_hits_match_c():
     b = _batch(0.06)
     T = kr.hit_threshold_lt(0.03)
-    P = kr.gap_thresholds(T, 121)
+    P = kr.gap_thresholds(T, kr.GAP_CHUNK)
     for ep in range(40):
         ek = kr.episode_key(0x5EED, 77, ep)
         for turn in range(0, 60, 7):
-            for n in (48, 121, 5, 0):
+            for n in (48, 121, 5, 0, 64, 65, 961):
                 assert kr.spawn_hits(ek, turn, n, P) == b.spawn_hits(ek, turn, n)
 
 
@@ -82,8 +82,8 @@ def test_spawn_sets_are_iid_bernoulli():
     q_chance = 0.2  # q = 0.1: enough hits for a tight check
     T = kr.hit_threshold_lt(q_chance / 2)
     q = T / 2**53
-    n = 48
-    P = kr.gap_thresholds(T, n)
+    n = 260  # three chunks (128, 128, 4)
+    P = kr.gap_thresholds(T, kr.GAP_CHUNK)
     counts = np.zeros(n)
     sizes = []
     N = 6000

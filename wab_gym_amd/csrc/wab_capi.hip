@@ -330,7 +330,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   split_threshold(bush_ge, &p.bush_th, &p.bush_tl);
   // keyed spawn sets (oracle/keyed_rng.py gap_thresholds): gap[g] = floor((1 - q)^g 2^53),
   // the power a running product in double (1 - q exact), so the oracle gets the same table
-  p.n_gap = p.R > p.WH ? p.R : p.WH;
+  p.n_gap = wab::kGapChunk;
   std::vector<uint64_t> gap_host((size_t)p.n_gap + 1);
   {
     const double omq = std::ldexp((double)((1ull << 53) - spawn_ge), -53);
@@ -341,8 +341,10 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
       gap_host[(size_t)g] = (uint64_t)std::floor(std::ldexp(q, 53));
     }
     p.gap_inv_l2 = spawn_ge > 0 ? (float)(1.0 / std::log2(omq)) : 0.0f;
-    split_threshold(gap_host[(size_t)p.R], &p.gap_ring_th, &p.gap_ring_tl);
-    split_threshold(gap_host[(size_t)p.WH], &p.gap_view_th, &p.gap_view_tl);
+    auto last_chunk = [](int n) { return n > 0 ? (n - 1) % wab::kGapChunk + 1 : 0; };
+    split_threshold(gap_host[(size_t)wab::kGapChunk], &p.gap_full_th, &p.gap_full_tl);
+    split_threshold(gap_host[(size_t)last_chunk(p.R)], &p.gap_ring_th, &p.gap_ring_tl);
+    split_threshold(gap_host[(size_t)last_chunk(p.WH)], &p.gap_view_th, &p.gap_view_tl);
   }
   p.fill = 1.0 / (double)c->turns_to_fill_food;
   p.hunger = 1.0 / (double)c->turns_to_empty_food;

@@ -128,22 +128,30 @@ __device__ __forceinline__ int gap_count_fast(const uint64_t* gap, int m, uint64
   return gap_count(gap, m, U);
 }
 
+// The tiles are taken in chunks of kGapChunk, each its own sequence (draw k of chunk c: "tile"
+// (k, c)), so that `gap` has kGapChunk + 1 entries; (thf, tlf) is gap[kGapChunk] split, (th, tl)
+// gap[m] of the last chunk.
 template <typename Hit>
-__device__ __forceinline__ void spawn_hits(const uint64_t* gap, int n, uint32_t th, uint32_t tl, float inv_l2,
-                                           int32_t turn, uint32_t b0, uint32_t b1, Hit&& hit) {
+__device__ __forceinline__ void spawn_hits(const uint64_t* gap, int n, uint32_t thf, uint32_t tlf, uint32_t th,
+                                           uint32_t tl, float inv_l2, int32_t turn, uint32_t b0, uint32_t b1,
+                                           Hit&& hit) {
   const uint32_t ts = make_ts(SITE_GAP, 0, turn);
-  const uint32_t h1 = fmix32(b0);  // "tile" (0, 0)
-  const uint32_t hi = fmix32(h1 ^ ts ^ b1);
-  if (n <= 0 || !U_ge(h1, hi, ts, b0, th, tl)) return;
-  uint64_t U = ((uint64_t)hi << 21) | draw_lo21(h1, ts, b0);
-  int pos = 0;
-  for (uint32_t k = 1;; ++k) {
-    const int G = gap_count_fast(gap, n - pos, U, inv_l2);
-    if (G >= n - pos) break;
-    pos += G;
-    hit(pos);
-    if (++pos >= n) break;
-    U = draw_U(xy_pack((int32_t)(k & 0xFFFFu), (int32_t)(k >> 16)), ts, b0, b1);
+  for (int c = 0, base = 0; base < n; ++c, base += kGapChunk) {  // (uniform)
+    const int m = min(kGapChunk, n - base);
+    const bool last = base + kGapChunk >= n;
+    const uint32_t h1 = fmix32(xy_pack(0, c) ^ b0);
+    const uint32_t hi = fmix32(h1 ^ ts ^ b1);
+    if (!U_ge(h1, hi, ts, b0, last ? th : thf, last ? tl : tlf)) continue;
+    uint64_t U = ((uint64_t)hi << 21) | draw_lo21(h1, ts, b0);
+    int pos = 0;
+    for (uint32_t k = 1;; ++k) {
+      const int G = gap_count_fast(gap, m - pos, U, inv_l2);
+      if (G >= m - pos) break;
+      pos += G;
+      hit(base + pos);
+      if (++pos >= m) break;
+      U = draw_U(xy_pack((int32_t)k, c), ts, b0, b1);
+    }
   }
 }
 

@@ -11,6 +11,7 @@ namespace wab {
 constexpr int kEnvsPerBlock = 64;   // env lanes = wave 0 of the block
 constexpr int kThreads = 256;       // 4 waves: waves 0..3 share the tile-parallel phases
 constexpr int kMaxWolfSlots = 32;
+constexpr int kGapChunk = 128;      // tiles per keyed spawn-set chunk (oracle/keyed_rng.py GAP_CHUNK)
 
 // device counters (Params::counters, read back by wab_get_counters; rare events: atomics)
 enum : int {
@@ -60,14 +61,16 @@ struct Params {
   // T = 2^53 ("never") is encoded (0xFFFFFFFF, 0xFFFFFFFF) which no (hi, lo21) reaches
   uint32_t keep_th, keep_tl;    // despawn: wolf kept iff U >= keep_gt + 1  (u > p, wab_env.py:263)
   uint32_t bush_th, bush_tl;    // bush present iff U >= T_1                 (wab_env.py:632-635)
-  // wolf spawns (u < p/2, wab_env.py:573, :590) are drawn as sets by geometric gaps
-  // (oracle/keyed_rng.py spawn_hits): gap[g] = floor((1 - q)^g 2^53), g = 0..n_gap; the
-  // first draw of a set is a miss of all n tiles iff U < gap[n], tested split like the above
-  const uint64_t* gap;          // device [n_gap + 1]
-  int32_t n_gap;                // max(R, WH)
+  // wolf spawns (u < p/2, wab_env.py:573, :590) are drawn as sets by geometric gaps in
+  // chunks of kGapChunk tiles (oracle/keyed_rng.py spawn_hits): gap[g] = floor((1 - q)^g
+  // 2^53), g = 0..kGapChunk; the first draw of a chunk of m tiles is a miss of all of them
+  // iff U < gap[m], tested split like the above for a full chunk and for the last one
+  const uint64_t* gap;          // device [kGapChunk + 1]
+  int32_t n_gap;                // kGapChunk (the tables' size)
   float gap_inv_l2;             // 1 / log2(1 - q) (the guess of gap_count_fast; the table decides)
-  uint32_t gap_ring_th, gap_ring_tl;  // gap[R]: no spawn on the ring this turn
-  uint32_t gap_view_th, gap_view_tl;  // gap[WH]: no initial wolf in the view
+  uint32_t gap_full_th, gap_full_tl;  // gap[kGapChunk]
+  uint32_t gap_ring_th, gap_ring_tl;  // gap[m] of the ring's last chunk
+  uint32_t gap_view_th, gap_view_tl;  // gap[m] of the view's last chunk
   const uint64_t* thresholds;  // device [max_berries] T_k
   const uint32_t* tables;      // device: [WH] view-cell world offsets (cw - i, ch - j), then from
   int32_t ring_at;             //   ring_at (16-B aligned) the R ring offsets, padded to a multiple of 4

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
         // this turn, one draw unless a wolf spawns (keyed spawn sets, wab_device.h)
         uint32_t* sm = spawnM + be * p.RW;
         if (sub == 0 && p.wolves_on)
-          spawn_hits(p.gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, (int32_t)(sn.w & 0xFFFFFu), kb0, sn.z,
+          spawn_hits(p.gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, (int32_t)(sn.w & 0xFFFFFu), kb0, sn.z,
                      [&](int r) { atomicOr(&sm[r >> 5], 1u << (r & 31)); });
         // the row or column that scrolled into view (generate_bushes :613-629)
         const int bdir = (int)(sn.w >> 24);
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       // initialize_wolves (:578-593): each job's view spawn set at turn 0, one thread per job
       if (p.wolves_on && tid < n_jobs) {
         const uint32_t je = jobEnv[tid];
-        spawn_hits(p.gap, WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, jobKey[2 * tid], jobKey[2 * tid + 1], [&](int c) {
+        spawn_hits(p.gap, WH, p.gap_full_th, p.gap_full_tl, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, jobKey[2 * tid], jobKey[2 * tid + 1], [&](int c) {
           lds_set(sB, je * (uint32_t)p.OB + tile_bit(tiles[c]));
           lds_set(wolfM + tid * p.WHW, (uint32_t)c);
         });

@@ -147,7 +147,7 @@ __device__ __forceinline__ void specialise_geometry(Params& p) {
     p.W = 11; p.H = 11; p.S = 11; p.cw = 5; p.ch = 5; p.margin = 1;
     p.OB = 363; p.WH = 121; p.R = 48; p.NT = 169; p.RW = 2; p.WHW = 4; p.SL = 11;
     p.ring_at = 124;
-    p.n_gap = 121;
+    p.n_gap = kGapChunk;
     p.small_masks[0][0] = 0x00400801u; p.small_masks[0][1] = 0x00801002u;  // column 0 (j = 0)
     p.small_masks[0][2] = 0x01002004u; p.small_masks[0][3] = 0x00004008u;
     p.small_masks[1][0] = 0x00200400u; p.small_masks[1][1] = 0x00400801u;  // column H-1
@@ -427,7 +427,7 @@ __device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, cons
                         : p.start_role;
   M128 nwm = {0ull, 0ull};
   if (p.wolves_on)
-    spawn_hits(s.gap, p.WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, kb0, kb1, [&](int c) { m_set(nwm, (uint32_t)c); });
+    spawn_hits(s.gap, p.WH, p.gap_full_th, p.gap_full_tl, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, kb0, kb1, [&](int c) { m_set(nwm, (uint32_t)c); });
   if (nwm.lo | nwm.hi) {
     const M128 wp = p.restrict_view ? m_andn(nwm, view_mask_of(p, role2)) : nwm;
     stream_or128(s.stream, ebit, wp);
@@ -954,7 +954,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   // spawn_wolves (:527-576): the ring's spawn set this turn (one draw unless a wolf spawns)
   M128 spawn = {0ull, 0ull};
   if (p.wolves_on && h.active)
-    spawn_hits(s.gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, b0, b1, [&](int r) { m_set(spawn, (uint32_t)r); });
+    spawn_hits(s.gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, b0, b1, [&](int r) { m_set(spawn, (uint32_t)r); });
   s.spawn[lane] = m_pack(spawn);
   s.strip[64 + lane] = strip_draws(p, h, b0, b1, kStripW1, 1 << 30);  // the entering strip, part 2
   SMALL_STAMP(23);
@@ -1002,15 +1002,25 @@ __device__ __forceinline__ void store_obs(const Params& p, const uint32_t* strea
   const uint32_t OB = (uint32_t)p.OB;
   const uint32_t limit = (uint32_t)min((int64_t)64, p.B - g0) * OB;
   uint8_t* out = p.planes + (size_t)g0 * OB;
-  // one 16-bit unit of the stream -> 16 bytes: each wave-instruction stores 1 KiB contiguous
+  // one 16-bit unit of the stream -> 16 bytes: each wave-instruction stores 1 KiB contiguous.
+  // A group has at most 64 * 384 bits (OB <= 3 * 128) = 1536 units: six per thread, all read
+  // from LDS before the first is expanded (a loop waits for each read in turn)
   const uint16_t* s16 = reinterpret_cast<const uint16_t*>(stream);
   const uint32_t full = limit >> 4;
-  for (uint32_t u = tid; u < full; u += 256) {
-    const uint32_t v = s16[u];
+  uint32_t v[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
+    v[k] = u < full ? (uint32_t)s16[u] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
+    if (u >= full) break;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     u32x4 q;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
     __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
   }
   for (uint32_t b = (full << 4) + tid; b < limit; b += 256)  // a partial last group

@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
           if (p.wolves_on && active)  // one draw unless a wolf spawns
-            spawn_hits(gap, p.R, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
+            spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
               spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
             });
           obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
       const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
       for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;
       if (p.wolves_on)
-        spawn_hits(MODE == MODE_STEP ? gap : p.gap, p.WH, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, (uint32_t)ek2,
+        spawn_hits(MODE == MODE_STEP ? gap : p.gap, p.WH, p.gap_full_th, p.gap_full_tl, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, (uint32_t)ek2,
                    (uint32_t)(ek2 >> 32), [&](int c) {
                      const uint32_t i = (uint32_t)c / (uint32_t)p.H;
                      wp[me + i] |= 1u << ((uint32_t)c - i * (uint32_t)p.H);
