@@ -239,6 +239,34 @@ __device__ __forceinline__ double sreg(double v) {
   return v;
 }
 
+// An opaque copy: whatever uses the value comes after this point.  Placed after a wave's last
+// load, it keeps the compiler from folding the first uses of each loaded value (a +1, a
+// mask) into the load's own block, where the wait for that load would stall the loads after
+// it (one s_waitcnt for all of them instead of one per group).  After a load made on one
+// path only, it also settles the wait there: the compiler otherwise treats the value as
+// possibly in flight at every later use and waits with vmcnt(0), which also waits for every
+// store the wave has issued since.
+template <typename T>
+__device__ __forceinline__ void opaque(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
+// A fresh copy of the kernel's parameter block, loaded from the kernel-argument segment
+// behind an opaque pointer: the scalar loads of the fields a block of code uses then stay in
+// that block.  (The kernel argument itself has every field loaded at the kernel's entry and,
+// past the SGPR budget, spilled to VGPR lanes; a copy per wave branch and per phase keeps
+// only what that branch uses live.)
+__device__ __forceinline__ Params kernel_params(const Params& p0) {
+#if __HIP_DEVICE_COMPILE__  // (the host pass only type-checks the kernel bodies)
+  typedef const Params __attribute__((address_space(4))) KernargParams;
+  KernargParams* pk = (KernargParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  return *pk;
+#else
+  return p0;
+#endif
+}
+
 // Per-lane choice between two wave-uniform 64-bit values by masks: the compiler turns a
 // plain ?: of two kernel-argument doubles into a scratch array indexed per lane.
 __device__ __forceinline__ uint64_t sel64(bool c, uint64_t a, uint64_t b) {

@@ -101,7 +101,7 @@ struct Params {
   uint8_t* eaten_rem;  // [cap][B] berries left
   uint32_t* bushmap;   // [WHW][B] bush presence of the current view, bit i*H + j (post-eat)
   unsigned long long* counters;      // [kNumCounters] (CTR_*)
-  unsigned long long* block_resets;  // [n_blocks]: resets done by each block (owned, no atomics)
+  unsigned long long* block_resets;  // [n_blocks]: resets done by each block (owned; no-return atomic adds)
   // ---- io (device, caller-owned)
   const int8_t* actions;
   const uint8_t* reset_mask;

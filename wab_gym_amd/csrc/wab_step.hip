@@ -571,7 +571,7 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
       }
       p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role, 0u, (uint32_t)n, 0u, 0u), ep);
     }
-    if (tid == 0) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
+    if (tid == 0) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);  // (no-return: a load here would wait for the stores)
     lds_barrier();
   }
   WAB_STAMP(5);

@@ -91,15 +91,7 @@ __device__ __forceinline__ HeadRaw head_fetch(const Params& p, int64_t g, bool a
   return r;
 }
 
-// An opaque copy: whatever uses the value comes after this point.  Placed after a wave's last
-// load, it keeps the compiler from folding the first uses of each loaded value (a +1, a
-// mask) into the load's own block, where the wait for that load would stall the loads after
-// it (one s_waitcnt for all of them instead of one per group).
-template <typename T>
-__device__ __forceinline__ void opaque(T& v) {
-  asm volatile("" : "+v"(v));
-}
-__device__ __forceinline__ void opaque(HeadRaw& r) {
+__device__ __forceinline__ void opaque_head(HeadRaw& r) {
   opaque(r.hdr.x);
   opaque(r.hdr.y);
   opaque(r.hdr.z);
@@ -505,7 +497,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
       lrem[i] = p.eaten_rem[at];
     }
   }
-  opaque(hr);
+  opaque_head(hr);
   opaque(food);
   opaque(bw0);
   opaque(bw1);
@@ -653,7 +645,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   if (active && !h.valid_action) atomicAdd(&p.counters[CTR_BAD_ACTIONS], 1ull);
   count_steps(p);
   const unsigned long long jm = __ballot(job);
-  if (lane == 0 && jm) p.block_resets[blockIdx.x] += (unsigned long long)__popcll(jm);
+  if (lane == 0 && jm) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)__popcll(jm));  // (no-return: a load here would wait for the stores)
   if (early_obs(p)) {
     lds_await(p, &s.flag[2]);  // S rendered (W2)
     store_units(p, s.stream, jm, false, 0, 3, lane);
@@ -702,7 +694,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     uint64_t tv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) tv[k] = p.thresholds[min(64 * k + lane, max(nthr, 1) - 1)];  // (>= 1 entry)
-    opaque(hr);
+    opaque_head(hr);
 #pragma unroll
     for (int k = 0; k < 4; ++k) opaque(tv[k]);
 #pragma unroll
@@ -776,7 +768,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
     for (int k = 0; k < kSpecSlots; ++k) wr[k] = p.wolves[(int64_t)k * p.B + gl];  // speculatively
   }
   HeadRaw hr = head_fetch(p, g, active);
-  opaque(hr);
+  opaque_head(hr);
 #pragma unroll
   for (int k = 0; k < kSpecSlots; ++k) opaque(wr[k]);
   const Head h = head_decode(p, g, active, hr);
@@ -931,7 +923,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
     uint64_t gv[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) gv[k] = p.gap[min(64 * k + lane, n - 1)];
-    opaque(hr);
+    opaque_head(hr);
 #pragma unroll
     for (int k = 0; k < 3; ++k) opaque(gv[k]);
 #pragma unroll

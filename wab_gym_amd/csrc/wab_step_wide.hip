@@ -247,12 +247,13 @@ __device__ __forceinline__ void obs_env_all(const Params& p, const uint32_t* bm,
 }  // namespace
 
 template <int MODE, int SLOTS>
-__global__ __launch_bounds__(256) void wab_step_wide(Params p) {
+__global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const Params p = kernel_params(p0);  // (re-read per wave branch and phase below)
   const WideLayout L = wide_layout(p);
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   if (g0 >= p.B) return;  // (uniform over the workgroup)
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int n_active = (int)min((int64_t)64, p.B - g0);
   const int64_t g = g0 + lane;
   const bool active = lane < n_active;
@@ -290,6 +291,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
 
     if (wave == 0) {
       // ------------------------------------------------ W0 P0: loads, despawn, pursuit, kill, wolf grid
+      const Params p = kernel_params(p0);
       __builtin_amdgcn_s_setprio(3);  // the longest chain
       uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
       if (active) {
@@ -311,6 +313,14 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
 #pragma unroll
       for (int k = 4; k < SLOTS; ++k)
         if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) opaque(wr[k]);  // (loaded on some paths only: settle it here)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        opaque(lxy[i]);
+        opaque(lrem[i]);
+      }
+      opaque(food);
       live = nw >= 32 ? ~0u : ((1u << nw) - 1u);
       // despawn (:262-264): one draw per wolf, keyed by its tile and its occurrence index
       // among the co-located wolves before it; groups of 4 slots
@@ -479,6 +489,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
         p.food[g] = food;
       }
     } else {
+      const Params p = kernel_params(p0);
       if (wave == 1) {
         // ---------------------------------------------- W1 P0: the view bitmap
         __builtin_amdgcn_s_setprio(2);
@@ -592,6 +603,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
   } else {
     // ------------------------------------------------ MODE_RESET: the flagged envs are jobs
     if (wave == 0) {
+      const Params p = kernel_params(p0);
       job = active && (p.reset_mask == nullptr || p.reset_mask[g] != 0);
       info[lane] = job ? 1u : 0u;
       const unsigned long long jm = __ballot(job);
@@ -612,6 +624,8 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
 
   const int n_jobs = (int)blk[0];
   const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+  {  // (the tail: its own parameter copy)
+  const Params p = kernel_params(p0);
   if constexpr (MODE == MODE_STEP) {
     // ------------------------------------------------ P2: bitmaps of the continuing envs (post-eat)
     for (uint32_t u = tid; u < 64u * 32u; u += 256) {  // env-major rows: 128 contiguous bytes per env
@@ -627,11 +641,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
     }
     if (wave == 0) {
       if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
-      if (lane == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
+      if (lane == 0 && n_jobs) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);  // (no-return: a load here would wait for the stores)
       count_steps(p);
     }
   } else {
-    if (tid == 0 && n_jobs) p.block_resets[blockIdx.x] += (unsigned long long)n_jobs;
+    if (tid == 0 && n_jobs) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);  // (no-return: a load here would wait for the stores)
   }
 
   if (n_jobs > 0) {
@@ -702,6 +716,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p) {
     }
   }
   if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
+  }
 #ifdef WAB_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   WIDE_STAMP(8 * wave + 6);
