@@ -507,6 +507,17 @@ void wabo_get_state(const wabo_batch* b, double* food, int32_t* x, int32_t* y, i
   }
 }
 
+/* Eaten-log lengths and the entries with no berries left (diagnostics: tools/). */
+void wabo_get_eaten_counts(const wabo_batch* b, int32_t* n_eaten, int32_t* n_emptied) {
+  for (int64_t i = 0; i < b->batch; ++i) {
+    const oenv* e = &b->envs[i];
+    int z = 0;
+    for (int k = 0; k < e->ne; ++k) z += e->eaten[k].rem == 0 ? 1 : 0;
+    n_eaten[i] = e->ne;
+    n_emptied[i] = z;
+  }
+}
+
 /* ------------------------------------------------------------------ config-5 featurizer */
 /* PragmaticObsWrapper.observation (wab_env.py:726-824) followed by gym 0.17 spaces.flatten
  * (actor_critic.py:188): Discrete(n) -> one-hot(n) float32, Tuple -> concatenation,

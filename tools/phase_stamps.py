@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--config", default="default")
     ap.add_argument("--build-only", action="store_true", help="build the stamps library and exit (CPU side)")
     ap.add_argument("--no-build", action="store_true", help="use the prebuilt stamps library (GPU box)")
+    ap.add_argument("--lib", default=OUT, help="the stamps library to load (with --no-build)")
     args = ap.parse_args()
     import __graft_entry__ as ge
 
@@ -31,7 +32,7 @@ def main():
         subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS", "-o", OUT] + src, check=True)
     if args.build_only:
         return
-    os.environ["WAB_LIB"] = OUT
+    os.environ["WAB_LIB"] = args.lib if args.no_build else OUT
     import numpy as np
     import torch
 
@@ -46,7 +47,7 @@ def main():
     L = _lib.load()
     L.wab_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     nb = (B + 63) // 64
-    st = torch.zeros((nb, 32), dtype=torch.int64, device="cuda:0")
+    st = torch.zeros((nb, 40), dtype=torch.int64, device="cuda:0")
     env.reset()
     L.wab_debug_set_stamps(env._h, st.data_ptr())
     g = torch.Generator(device="cuda:0")
@@ -170,7 +171,8 @@ def small_report(env, st, g, steps):
                                                    "obs stores"])}
     acc = {k: [] for k in waves}
     spans, ends = [], []
-    by_xcd, slow_w0, fast_w0, start_off = [], [], [], []
+    by_xcd, slow_w0, fast_w0, start_off, start_xcd, quart = [], [], [], [], [], []
+    entry_xcd, first_xcd, w0_lag, xmap = [], [], [], []
     # extra stamps: W2 28 after B_init, 29 after despawn; W1 30 after B_init, 31 after the key;
     # W3 24 after its reset draws, 9 after the wait for W1's (groups without a done env
     # leave 24 and 9 at 0: only groups with one are averaged)
@@ -186,7 +188,7 @@ def small_report(env, st, g, steps):
         if t < 20:
             continue
         s = st.cpu().numpy().astype(np.int64)[:nb]
-        t0 = min(s[:, 0].min(), s[:, 10].min(), s[:, 16].min(), s[:, 22].min())
+        t0 = min(s[:, 0].min(), s[:, 10].min(), s[:, 16].min(), s[:, 22].min(), s[:, 32].min())
         for k, (cols, _) in waves.items():
             acc[k].append(np.diff(s[:, cols], axis=1).mean(axis=0))
         end = s[:, [6, 15, 21, 27]].max(axis=1)
@@ -194,6 +196,14 @@ def small_report(env, st, g, steps):
         ends.append(np.percentile(end - t0, [0, 50, 100]))
         xcd = np.arange(len(end)) % 8
         by_xcd.append([(end - t0)[xcd == x].mean() for x in range(8)])
+        start0 = s[:, [0, 10, 16, 22]].min(axis=1) - t0
+        start_xcd.append([start0[xcd == x].mean() for x in range(8)])
+        quart.append([q.mean() for q in np.array_split(end - t0, 4)])
+        xc = s[:, 33] & 7
+        entry_xcd.append([(s[xc == x, 32] - t0).mean() for x in range(8)])
+        first_xcd.append([(s[xc == x, 32] - t0).min() for x in range(8)])
+        w0_lag.append([(s[xc == x, 0] - s[xc == x, 32]).mean() for x in range(8)])
+        xmap.append((xc == (np.arange(len(xc)) % 8)).mean())
         order = np.argsort(end)
         cols0 = waves["W0 bushes"][0]
         d0 = np.diff(s[:, cols0], axis=1)
@@ -214,6 +224,12 @@ def small_report(env, st, g, steps):
     print("%-24s %7.2f us (first start -> last end)" % ("launch span", np.mean(spans) * 10 / 1000))
     print("workgroup end times p0/p50/max (us):", np.round(np.mean(ends, axis=0) * 10 / 1000, 2))
     print("mean end time by blockIdx %% 8 (us):", np.round(np.mean(by_xcd, axis=0) * 10 / 1000, 2))
+    print("mean start time by blockIdx %% 8 (us):", np.round(np.mean(start_xcd, axis=0) * 10 / 1000, 2))
+    print("mean end time by blockIdx quartile (us):", np.round(np.mean(quart, axis=0) * 10 / 1000, 2))
+    print("XCC_ID == blockIdx %% 8 for %.1f %% of workgroups" % (100 * np.mean(xmap)))
+    print("kernel entry by XCC, first / mean (us):", np.round(np.mean(first_xcd, axis=0) * 10 / 1000, 2),
+          np.round(np.mean(entry_xcd, axis=0) * 10 / 1000, 2))
+    print("entry -> W0 first stamp by XCC (us):", np.round(np.mean(w0_lag, axis=0) * 10 / 1000, 2))
     print("W0 phases, slowest 5%% of workgroups (us):", np.round(np.mean(slow_w0, axis=0) * 10 / 1000, 2))
     print("W0 phases, fastest 25%% of workgroups (us):", np.round(np.mean(fast_w0, axis=0) * 10 / 1000, 2))
     print("W0 start offset slowest 5%% / fastest 25%% (us):", np.round(np.mean(start_off, axis=0) * 10 / 1000, 2))

@@ -116,7 +116,7 @@ struct Params {
   uint8_t* t_role;
   uint8_t* t_status;
   float* features;     // wab_step_features: PragmaticObsWrapper features [B][F] (else null)
-  unsigned long long* stamps;  // diagnostic builds only (-DWAB_STAMPS): [n_blocks][16] s_memrealtime
+  unsigned long long* stamps;  // diagnostic builds only (-DWAB_STAMPS): [n_blocks][40] s_memrealtime
 };
 
 // LDS carve of one workgroup (dword offsets, each region 16-byte aligned).

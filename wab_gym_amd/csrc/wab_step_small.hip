@@ -39,14 +39,14 @@
 namespace wab {
 
 // Diagnostic build (-DWAB_STAMPS): lane 0 of each wave records s_memrealtime (100 MHz) at
-// phase boundaries into p.stamps[workgroup * 32 + slot] (W0 0..9, W1 10..15, W2 16..21, W3 22..27):
+// phase boundaries into p.stamps[workgroup * 40 + slot] (W0 0..9, W1 10..15, W2 16..21, W3 22..27):
 // a wave's stamps k, k+1, k+2, k+3 close its phases P0..P3 (the barrier waits sit at the
 // start of the next phase), the last one the retirement of its obs stores.
 #ifdef WAB_STAMPS
 #define SMALL_STAMP(slot)                                                                \
   do {                                                                                   \
     if (lane == 0 && p.stamps)                                                           \
-      p.stamps[(size_t)blockIdx.x * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 #else
 #define SMALL_STAMP(slot) do {} while (0)
@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void store_obs(const Params& p, const uint32_t* strea
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if ((tid & 63) == 0 && p.stamps) {
     const int slot[4] = {6, 15, 21, 27};
-    p.stamps[(size_t)blockIdx.x * 32 + slot[tid >> 6]] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(size_t)blockIdx.x * 40 + slot[tid >> 6]] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
@@ -1087,6 +1087,14 @@ template <int SLOTS, int G, bool FEAT>
 __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if ((int64_t)blockIdx.x * 64 >= p0.B) return;  // (uniform over the workgroup)
+#ifdef WAB_STAMPS
+  if (threadIdx.x == 0 && p0.stamps) {  // kernel entry (slot 32) and the XCD (slot 33)
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    p0.stamps[(size_t)blockIdx.x * 40 + 32] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
+  }
+#endif
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (uniform branches)
   unsigned long long jm;  // the group's done envs (every wave computes the same mask)
 #ifdef WAB_ONLY_WAVE  // static per-wave instruction counts (tools/isa_count.py); not a runnable build

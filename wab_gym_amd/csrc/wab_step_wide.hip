@@ -40,7 +40,7 @@ namespace wab {
 #define WIDE_STAMP(slot)                                                                 \
   do {                                                                                   \
     if (lane == 0 && p.stamps)                                                           \
-      p.stamps[(size_t)blockIdx.x * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 #else
 #define WIDE_STAMP(slot) do {} while (0)
