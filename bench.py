@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--mode", default="graph", choices=["graph", "launch"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
+                    help="override the config's wolf slot capacity (0: the config's own)")
     ap.add_argument("--c5-unfused", action="store_true",
                     help="C5 as wab_step + wab_featurize (obs planes stored) instead of wab_step_features")
     args = ap.parse_args()
@@ -170,6 +172,7 @@ def main():
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
 
     opts, stride, slots, desc = CONFIGS[args.config]
+    slots = args.wolf_slots or slots
     c5 = args.config == "c5"
     B, K, W = args.batch, args.steps, args.warmup
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
@@ -359,7 +362,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic: uniform random actions (torch.randint on device), keyed-RNG worlds",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B * world,
-                       "viewport": [Wv, Hv], "plane_stride": env.S, "launch": args.mode,
+                       "viewport": [Wv, Hv], "plane_stride": env.S, "wolf_slots": slots, "launch": args.mode,
                        "parallelism": "independent env shards x%d (no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

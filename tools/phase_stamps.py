@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--build-only", action="store_true", help="build the stamps library and exit (CPU side)")
     ap.add_argument("--no-build", action="store_true", help="use the prebuilt stamps library (GPU box)")
     ap.add_argument("--lib", default=OUT, help="the stamps library to load (with --no-build)")
+    ap.add_argument("--b2b", type=int, default=0,
+                    help="instead: per-XCD entry/end of the last two of N back-to-back launches")
     args = ap.parse_args()
     import __graft_entry__ as ge
 
@@ -53,6 +55,8 @@ def main():
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     kind = env.step_kernel
+    if args.b2b:
+        return b2b_report(env, L, g, args.steps, args.b2b)
     if kind == "small":
         return small_report(env, st, g, args.steps)
     if kind == "wide":
@@ -151,6 +155,53 @@ def wide_report(env, st, g, steps):
     for name, idx in (("fastest 10%", order[: nb // 10]), ("slowest 10%", order[-nb // 10:])):
         print("  %s: obs start %.2f, obs issue %.2f, drain %.2f, end %.2f us" % (
             name, us((s[idx, 10] - t0).mean()), us(obs[idx].mean()), us((s[idx, 14] - s[idx, 13]).mean()), us(e_[idx].mean())))
+
+
+def b2b_report(env, L, g, steps, n):
+    """Back-to-back launches as the bench issues them (no synchronisation in between): each
+    launch stamps into one of two buffers, alternately; per XCD (the XCC_ID register) the mean
+    kernel-entry offset of the last launch's workgroups from its first one, its mean and last
+    workgroup end, and the gap from the previous launch's last workgroup end to the first
+    entry of the last launch.  Slots: 32 entry, 33 XCC_ID; ends: the small kernel's obs-store
+    stamps 6/15/21/27, the wide kernel's 6/14/22/30."""
+    import numpy as np
+    import torch
+
+    B = env.num_envs
+    nb = (B + 63) // 64
+    bufs = [torch.zeros((nb, 40), dtype=torch.int64, device="cuda:0") for _ in range(2)]
+    ends_cols = [6, 15, 21, 27] if env.step_kernel == "small" else [6, 14, 22, 30]
+    acts = torch.randint(0, env.n_actions, (n, B), device="cuda:0", generator=g).to(torch.int8)
+    entry, endx, lastx, gaps, spans, karg = [], [], [], [], [], []
+    for t in range(steps):
+        for b in bufs:
+            b.zero_()
+        torch.cuda.synchronize()
+        for i in range(n):
+            L.wab_debug_set_stamps(env._h, bufs[i % 2].data_ptr())
+            env.step(acts[i])
+        torch.cuda.synchronize()
+        last = bufs[(n - 1) % 2].cpu().numpy().astype(np.int64)[:nb]
+        prev = bufs[(n - 2) % 2].cpu().numpy().astype(np.int64)[:nb]
+        t0 = last[:, 32].min()
+        xc = last[:, 33] & 7
+        end = last[:, ends_cols].max(axis=1) - t0
+        entry.append([(last[xc == x, 32] - t0).mean() for x in range(8)])
+        endx.append([end[xc == x].mean() for x in range(8)])
+        lastx.append([end[xc == x].max() for x in range(8)])
+        gaps.append(t0 - prev[:, ends_cols].max())
+        if env.step_kernel == "small":
+            karg.append([(last[xc == x, 34] - last[xc == x, 32]).mean() for x in range(8)])
+        spans.append(end.max())
+    us = lambda v: np.round(np.mean(v, axis=0) * 10 / 1000, 2)
+    print("back-to-back launches: %d x %d, last two stamped" % (steps, n))
+    print("entry by XCC, mean (us):   ", us(entry))
+    print("end by XCC, mean (us):     ", us(endx))
+    print("end by XCC, last (us):     ", us(lastx))
+    print("launch span (us):          ", us(spans))
+    print("previous last end -> first entry (us):", us(gaps))
+    if karg:
+        print("entry -> first kernel-argument field by XCC (us):", us(karg))
 
 
 def small_report(env, st, g, steps):

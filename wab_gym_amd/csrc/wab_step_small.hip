@@ -1086,12 +1086,17 @@ __device__ __forceinline__ Params wave_params(const Params& p0) {
 template <int SLOTS, int G, bool FEAT>
 __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+#ifdef WAB_STAMPS
+  uint64_t t_entry;  // before the first kernel-argument load
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry)::"memory");
+#endif
   if ((int64_t)blockIdx.x * 64 >= p0.B) return;  // (uniform over the workgroup)
 #ifdef WAB_STAMPS
-  if (threadIdx.x == 0 && p0.stamps) {  // kernel entry (slot 32) and the XCD (slot 33)
+  if (threadIdx.x == 0 && p0.stamps) {  // kernel entry (slot 32), the XCD (33), first kernarg field in (34)
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    p0.stamps[(size_t)blockIdx.x * 40 + 32] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * 40 + 34] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * 40 + 32] = t_entry;
     p0.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
   }
 #endif

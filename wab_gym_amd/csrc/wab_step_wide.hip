@@ -251,8 +251,20 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const Params p = kernel_params(p0);  // (re-read per wave branch and phase below)
   const WideLayout L = wide_layout(p);
+#ifdef WAB_WIDE_ROT  // diagnostic: rotate the workgroup -> env-chunk mapping (XCD vs address effects)
+  const int64_t g0 = (int64_t)((blockIdx.x + WAB_WIDE_ROT) % gridDim.x) * 64;
+#else
   const int64_t g0 = (int64_t)blockIdx.x * 64;
+#endif
   if (g0 >= p.B) return;  // (uniform over the workgroup)
+#ifdef WAB_STAMPS
+  if (threadIdx.x == 0 && p.stamps) {  // kernel entry (slot 32) and the XCD (slot 33)
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    p.stamps[(size_t)blockIdx.x * 40 + 32] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
+  }
+#endif
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int n_active = (int)min((int64_t)64, p.B - g0);
   const int64_t g = g0 + lane;
