@@ -76,6 +76,24 @@ static float time_graph(K kern, Bufs b, int steps, int blocks = 1024, int thread
   return ms * 1000.0f / (float)steps;
 }
 
+template <typename K>
+static float time_stream(K kern, Bufs b, int steps, int blocks = 1024, int threads = 256, int lds = 14336) {
+  hipStream_t s;
+  (void)hipStreamCreate(&s);
+  for (int i = 0; i < 50; ++i) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), lds, s, b);
+  (void)hipStreamSynchronize(s);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, s);
+  for (int i = 0; i < steps; ++i) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), lds, s, b);
+  (void)hipEventRecord(e1, s);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1000.0f / (float)steps;
+}
+
 int main() {
   const size_t B = 65536;
   Bufs b;
@@ -98,6 +116,9 @@ int main() {
   printf("empty 256x256    %.3f us/launch\n", time_graph(k_empty, b, 4000, 256, 256, 14336));
   printf("empty 1x64       %.3f us/launch\n", time_graph(k_empty, b, 4000, 1, 64, 0));
   printf("mem        %.3f us/launch\n", time_graph(k_mem<0>, b, 4000));
+  printf("empty 1024x256 stream launches  %.3f us/launch\n", time_stream(k_empty, b, 4000));
+  printf("mem stream launches             %.3f us/launch\n", time_stream(k_mem<0>, b, 4000));
+  printf("chain 100 stream launches       %.3f us/launch\n", time_stream(k_mem<100>, b, 4000));
   printf("chain 100  %.3f us/launch\n", time_graph(k_mem<100>, b, 4000));
   printf("chain 400  %.3f us/launch\n", time_graph(k_mem<400>, b, 4000));
   printf("chain 1000 %.3f us/launch\n", time_graph(k_mem<1000>, b, 4000));

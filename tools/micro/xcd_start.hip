@@ -63,6 +63,28 @@ __global__ __launch_bounds__(256) void k_small(uint64_t* t, uint32_t* xcc, int s
   if (v == 0xFFFFFFFEu) t[0] = lds[(threadIdx.x + 1) & 255];
 }
 
+// the step's stores after the spin: `words` 16-byte stores per thread (non-temporal or plain)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ __launch_bounds__(256) void k_store(uint64_t* t, uint32_t* xcc, int spin, u32x4* out, int words) {
+  uint64_t t0;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  if (threadIdx.x == 0) {
+    t[blockIdx.x] = t0;
+    uint32_t id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
+    xcc[blockIdx.x] = id & 0xFu;
+  }
+  uint32_t v = threadIdx.x;
+  for (int i = 0; i < spin; ++i) v = v * 1664525u + 1013904223u;
+  u32x4* o = out + (size_t)blockIdx.x * 256 * words;
+  for (int k = 0; k < words; ++k) {
+    const u32x4 q = {v, v + 1, v + 2, v + (uint32_t)k};
+    if (NT) __builtin_nontemporal_store(q, o + k * 256 + threadIdx.x);
+    else o[k * 256 + threadIdx.x] = q;
+  }
+}
+
 static const int nb = 1024, reps = 40;
 
 static void report(const char* name, uint64_t* t, uint32_t* x) {
@@ -95,6 +117,8 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&x, nb * 4 * reps);
   hipStream_t s;
   (void)hipStreamCreate(&s);
+  u32x4* out;
+  (void)hipMalloc(&out, (size_t)nb * 256 * 6 * 16);  // 24 MB: the step's obs bytes
   Big b{};
   b.spin = spin;
   for (int pass = 0; pass < 2; ++pass) {
@@ -133,6 +157,21 @@ int main(int argc, char** argv) {
     (void)hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphLaunch(exec, s);
     report("16 B args, graph", t, x);
+    for (int r = 0; r < reps; ++r)
+      hipLaunchKernelGGL(k_store<true>, dim3(nb), dim3(256), 14336, s, t + r * nb, x + r * nb, spin, out, 6);
+    report("24 MB nt stores, stream", t, x);
+    for (int r = 0; r < reps; ++r)
+      hipLaunchKernelGGL(k_store<false>, dim3(nb), dim3(256), 14336, s, t + r * nb, x + r * nb, spin, out, 6);
+    report("24 MB plain stores, stream", t, x);
+    for (int r = 0; r < reps; ++r)
+      hipLaunchKernelGGL(k_store<false>, dim3(nb), dim3(256), 14336, s, t + r * nb, x + r * nb, spin, out, 1);
+    report("4 MB plain stores, stream", t, x);
+    for (int r = 0; r < reps; ++r)
+      hipLaunchKernelGGL(k_store<false>, dim3(nb), dim3(256), 14336, s, t + r * nb, x + r * nb, 40, out, 6);
+    report("24 MB plain, short spin", t, x);
+    for (int r = 0; r < reps; ++r)
+      hipLaunchKernelGGL(k_store<true>, dim3(nb), dim3(256), 14336, s, t + r * nb, x + r * nb, 40, out, 6);
+    report("24 MB nt, short spin", t, x);
   }
   return 0;
 }

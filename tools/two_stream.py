@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--shards", type=int, default=2)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--join-every", type=int, default=1, help="fork/join every n steps")
+    ap.add_argument("--features", action="store_true",
+                    help="C5's fused wab_step_features into a [32, n, F] buffer per shard instead of wab_step")
     args = ap.parse_args()
     import torch
 
@@ -36,6 +38,12 @@ def main():
     actions = torch.randint(0, 5, (K + 50, B), device=dev, generator=gen).to(torch.int8)
     L = _lib.load()
     main_s = torch.cuda.current_stream(dev)
+    F = int(L.wab_feature_dim(envs[0]._h))
+    feats = [torch.empty((32, n, F), dtype=torch.float32, device=dev) if args.features else None for _ in range(S)]
+    fobs = []
+    for e in envs:
+        o = e._obs["struct"]
+        fobs.append(_lib.WabObs(None, o.food_turns, o.role, o.status))
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
 
     def step_all(t0, cnt):
@@ -46,8 +54,13 @@ def main():
                 st.wait_event(ev)
                 for u in range(t, min(t + args.join_every, t0 + cnt)):
                     a = actions[u, i * n:(i + 1) * n]
-                    _lib.check(L.wab_step(e._h, a.data_ptr(), ctypes.addressof(e._obs["struct"]), e.reward.data_ptr(),
-                                          e.done.data_ptr(), None, ctypes.c_void_p(st.cuda_stream)), "wab_step")
+                    if args.features:
+                        _lib.check(L.wab_step_features(e._h, a.data_ptr(), ctypes.addressof(fobs[i]), e.reward.data_ptr(),
+                                                       e.done.data_ptr(), feats[i][u % 32].data_ptr(),
+                                                       ctypes.c_void_p(st.cuda_stream)), "wab_step_features")
+                    else:
+                        _lib.check(L.wab_step(e._h, a.data_ptr(), ctypes.addressof(e._obs["struct"]), e.reward.data_ptr(),
+                                              e.done.data_ptr(), None, ctypes.c_void_p(st.cuda_stream)), "wab_step")
             for st in streams:
                 torch.cuda.current_stream(dev).wait_stream(st)
 
