@@ -46,6 +46,10 @@ namespace wab {
 #define WIDE_STAMP(slot) do {} while (0)
 #endif
 
+#ifndef WAB_WIDE_SPEC  // wolf slots W0 loads with the state, before the count is known
+#define WAB_WIDE_SPEC 8
+#endif
+
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
       if (active) {
         food = p.food[g];
 #pragma unroll
-        for (int k = 0; k < 4 && k < SLOTS; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
+        for (int k = 0; k < WAB_WIDE_SPEC && k < SLOTS; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (i < p.eaten_cap) {
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
       ndep = (int)misc_ndep(h.hdr.z);
       const int status_old = (int)misc_status(h.hdr.z);
 #pragma unroll
-      for (int k = 4; k < SLOTS; ++k)
+      for (int k = WAB_WIDE_SPEC; k < SLOTS; ++k)
         if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
 #pragma unroll
       for (int k = 0; k < SLOTS; ++k) opaque(wr[k]);  // (loaded on some paths only: settle it here)
