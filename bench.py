@@ -139,9 +139,60 @@ def cpu_baseline(opts, stride, seconds, threads, with_features=False):
                       "oracle/wab_oracle.c %s, %d envs x %d steps (%.1f s), 1 thread" % (what, Bc, n, el)}
 
 
+def probe_device_count():
+    """GPUs visible to a fresh process, counted in a child so this (launcher) process never
+    touches the GPU runtime before it starts the ranks."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        raise SystemExit("bench.py: could not count GPUs: %s" % r.stderr[-2000:])
+
+
+def self_launch(args):
+    """`bench.py --gpus N` run without a torch.distributed launcher (WORLD_SIZE unset): start N
+    fresh rank processes of this script, one per GPU (RANK = LOCAL_RANK = r), wait for all,
+    print rank 0's JSON line and return the first failing child's exit code.  Nothing here
+    touches the GPU: the device count comes from a child process."""
+    from wab_gym_amd.shard import launch_ranks
+
+    n = args.gpus
+    ndev = probe_device_count()
+    if n > ndev and not args.share_gpu:
+        raise SystemExit("bench.py: --gpus %d but %d GPU(s) visible; pass --share-gpu to run "
+                         "%d ranks on the visible GPU(s) (a rehearsal, not a scaling figure)" % (n, ndev, n))
+    rc, out, codes = launch_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], n)
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    for ln in out.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if rc != 0:
+        print("bench.py: rank exit codes %s" % codes, file=sys.stderr)
+        return rc if rc > 0 else 1
+    if not lines:
+        print("bench.py: rank 0 printed no JSON line", file=sys.stderr)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+def pci_id(dev):
+    """domain:bus:device of a torch device (tells ranks on distinct GPUs from shared ones)."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    return "%04x:%02x:%02x" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="allow --gpus N above the visible GPU count: ranks then share GPUs "
+                         "(rank r on GPU r mod count); a rehearsal of the N-rank path")
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--batch", type=int, default=65536)
@@ -154,6 +205,10 @@ def main():
     ap.add_argument("--c5-unfused", action="store_true",
                     help="C5 as wab_step + wab_featurize (obs planes stored) instead of wab_step_features")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
 
     import torch
     import torch.distributed as dist
@@ -161,8 +216,15 @@ def main():
     from wab_gym_amd.shard import all_gather_objects, env_id_base, max_over_ranks, rank_info
 
     rank, world, local = rank_info()
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d; the line reports WORLD_SIZE" % (args.gpus, world),
+              file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    if world > ndev and not args.share_gpu and local >= ndev:
+        raise SystemExit("bench.py: rank %d has no GPU of its own (%d visible); pass --share-gpu"
+                         % (rank, ndev))
     # ranks share a GPU when there are fewer GPUs than ranks (the 1-GPU rehearsal of N > 1)
-    local = local % max(1, torch.cuda.device_count())
+    local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -291,33 +353,50 @@ def main():
     alg = alg_bytes_per_env_step(env.W, env.H)
     c5_line = None
     if c5:
-        # C5 runs three kernels; each one's average launch comes from back-to-back launches of
-        # that kernel alone (HIP events on the launch stream, after the timed region)
+        # C5 runs three kernels; each one's average launch comes from n back-to-back launches of
+        # that kernel alone, captured in a graph (as the timed region is) so that host launch
+        # cost does not pace a short kernel; HIP events on the launch stream around one replay
         def per_launch(fn, n):
+            def launches(st):
+                sc = ctypes.c_void_p(st.cuda_stream)
+                for i in range(n):
+                    _lib.check(fn(i, sc), "c5 kernel timing")
+            if args.mode == "graph":
+                g = torch.cuda.CUDAGraph()
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(stream)
+                with torch.cuda.stream(side):
+                    with torch.cuda.graph(g, stream=side):
+                        launches(torch.cuda.current_stream(dev))
+                stream.wait_stream(side)
+                g.replay()  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for i in range(n):
-                _lib.check(fn(i), "c5 kernel timing")
+            if args.mode == "graph":
+                g.replay()
+            else:
+                launches(stream)
             e1.record(stream)
             torch.cuda.synchronize(dev)
             return e0.elapsed_time(e1) / n
 
         n_k = min(K, 512)
-        ret_ms = per_launch(lambda i: L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s), 64)
+        ret_ms = per_launch(lambda i, s: L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s), 64)
         if fused:
-            sf_ms = per_launch(lambda i: L.wab_step_features(h, a0 + (W + i) * B, fobs_addr, rew, done,
-                                                             f0 + 4 * (i % T) * B * F, s), n_k)
+            sf_ms = per_launch(lambda i, s: L.wab_step_features(h, a0 + (W + i) * B, fobs_addr, rew, done,
+                                                                f0 + 4 * (i % T) * B * F, s), n_k)
             # per env-step: the step's bytes without the planes (never stored), the F floats
             sf_alg = alg - 3 * env.W * env.H + 4 * F
             c5_line = {"segment": T, "feature_dim": F, "fused": True,
                        "step_features_us": round(sf_ms * 1e3, 3),
                        "returns_us_per_segment": round(ret_ms * 1e3, 3),
+                       "returns_frac": round(RETURNS_ALG_BYTES * T * B / (ret_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                        "alg_bytes_per_env_step": sf_alg + RETURNS_ALG_BYTES,
                        "achieved_GBs_whole_step": round((sf_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
             kernel_name = "wab_step_%s + PragmaticObsWrapper features (wab_step_features)" % L.wab_step_kernel(h).decode()
             alg, kern_ms = sf_alg, sf_ms
-        step_ms = per_launch(lambda i: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_k)
-        feat_ms = per_launch(lambda i: L.wab_featurize(h, obs_addr, None, f0 + 4 * (i % T) * B * F, s), n_k)
+        step_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_k)
+        feat_ms = per_launch(lambda i, s: L.wab_featurize(h, obs_addr, None, f0 + 4 * (i % T) * B * F, s), n_k)
         feat_alg = featurize_alg_bytes(env.W, env.H, F)
         if fused:
             c5_line["unfused_step_us"] = round(step_ms * 1e3, 3)
@@ -336,7 +415,7 @@ def main():
     counters = env.counters()
     achieved_rank = alg * B / (kern_ms * 1e-3) / 1e9
     per_rank = all_gather_objects({
-        "rank": rank, "device": str(dev), "env_steps_per_s": round(B * K / elapsed_rank, 1),
+        "rank": rank, "device": str(dev), "pci": pci_id(dev), "env_steps_per_s": round(B * K / elapsed_rank, 1),
         "ms_per_step": round(elapsed_rank * 1e3 / K, 5), "kernel_us": round(kern_ms * 1e3, 3),
         "achieved_GBs": round(achieved_rank, 1), "frac": round(achieved_rank / HBM_PEAK_GBS, 4),
         "timed_window": window, "overflow": counters["wolf_overflow"] + counters["eaten_overflow"],
@@ -383,8 +462,11 @@ def main():
         valu = committed_pmc(args.config, B) if not args.c5_unfused else None
         if valu:
             line["roofline"]["valu"] = valu
+        line["devices"] = sorted({r["pci"] for r in per_rank})
         if world > 1:
             line["per_rank"] = per_rank
+            if len(line["devices"]) < world:
+                line["shared_gpus"] = True  # a rehearsal: ranks share a GPU, not a scaling figure
         if c5:
             line["c5"] = c5_line
         else:

@@ -90,9 +90,10 @@ typedef struct wab_config {
   int32_t wolf_slots;              /* live-wolf slots per env: 8 (0 = 8), 16 or 32; a spawn
                                     * beyond them is dropped and counted (wolf_overflow) */
   /* T_k (k = 1..max_berries_per_bush): the smallest 53-bit U with
-   * round((U * 2^-53) ** bush_power * max_berries_per_bush) >= k, computed by the
-   * host with the reference's own numpy arithmetic (wab_env.py:632-635).
-   * Copied at wab_create. */
+   * round((U * 2^-53) ** bush_power * max_berries_per_bush) >= k (wab_env.py:632-635).
+   * Copied at wab_create.  NULL: wab_create computes it with wab_bush_thresholds (libm);
+   * the Python host passes the table of the reference's own numpy arithmetic
+   * (wab_gym_amd.options.bush_thresholds; the two agree on every option set tested). */
   const uint64_t* bush_thresholds;
 } wab_config;
 
@@ -137,6 +138,12 @@ const char* wab_last_error(void);
 /* Number of actions of the table selected by the options (5 or 6, wab_env.py:149-182). */
 int wab_num_actions(const wab_config* cfg);
 
+/* The bush-value threshold table of wab_config.bush_thresholds, in C: out[k-1] = the
+ * smallest U in [1, 2^53] with nearbyint(pow(U * 2^-53, bush_power) * max_berries) >= k
+ * (generate_n_bush_values, wab_env.py:631-635; 2^53 = no draw reaches k), by bisection
+ * over the 2^53 grid.  Host only, synchronous, no device needed. */
+int wab_bush_thresholds(double bush_power, int32_t max_berries, uint64_t* out);
+
 /* Validate options and allocate state for `batch` envs on HIP device `device`.
  * Env i has global id env_id_base + i; every random draw is keyed by
  * (seed, global id, episode, ...), so results do not depend on batch size, shard
@@ -180,8 +187,10 @@ int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* 
 /* Batch size of a handle. */
 int64_t wab_batch(const wab_handle* h);
 
-/* Name of the kernel wab_step launches for this handle ("small": the four-wave kernel for
- * views of at most 128 cells; "block": the general one).  Diagnostics only. */
+/* Name of the kernel wab_step launches for this handle: "small" (the four-wave kernel for
+ * views of at most 128 cells in unpadded rows), "wide" (views of at most 32x32 cells in rows
+ * of 16 or 32 bytes, without restrict_view: the 31x31 configuration) or "block" (the general
+ * one).  Diagnostics only. */
 const char* wab_step_kernel(const wab_handle* h);
 
 /* ---- config 5 (actor_critic.py rollout) ------------------------------------------ */

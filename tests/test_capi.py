@@ -1,6 +1,7 @@
 """The C-ABI library builds, loads without a GPU, exports every symbol include/wab.h declares,
 and its ctypes mirrors have the C layout (no compute calls here: those are -m gpu)."""
 import ctypes
+import math
 import os
 import re
 import subprocess
@@ -62,3 +63,45 @@ def test_ctypes_layout_matches_c(tmp_path):
         assert int(out[1 + i]) == getattr(WabConfig, f).offset, f
     assert int(out[-2]) == ctypes.sizeof(_lib.WabObs)
     assert int(out[-1]) == ctypes.sizeof(_lib.WabCounters)
+
+
+# (bush_power, max_berries): the defaults, every golden / parity option set, and edge cases
+THRESHOLD_CASES = [(100, 200), (60, 200), (20, 200), (400, 200), (20, 1), (2.5, 7), (1, 255),
+                   (400, 50), (100, 255), (1, 1), (0.5, 3), (100, 0)]
+
+
+@pytest.mark.parametrize("power,mx", THRESHOLD_CASES)
+def test_c_bush_thresholds_equal_numpy_table(power, mx):
+    """wab_bush_thresholds (C, libm) == options.bush_thresholds (the reference's numpy
+    expression, wab_env.py:631-635): a C caller can build wab_config without Python."""
+    import numpy as np
+
+    from wab_gym_amd.options import bush_thresholds
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libwab_hip.so not built")
+    L = _lib.load()
+    out = np.zeros(max(mx, 1), np.uint64)
+    assert L.wab_bush_thresholds(float(power), mx, out.ctypes.data) == 0
+    c, ref = out[:mx].astype(np.int64), bush_thresholds(power, mx).astype(np.int64)
+    # Equal, except where numpy's vectorised float64 pow (this numpy 2.2) is one ulp below
+    # libm's pow at the last draw before the boundary: the C table then starts one draw (2^-53)
+    # earlier.  The reference's pinned numpy 1.19 evaluates np.power with libm's pow, so there
+    # the C table is the reference's; the default options (100, 200) agree exactly.
+    for k in np.nonzero(c != ref)[0]:
+        U = int(c[k])
+        assert U == ref[k] - 1, (k, U, ref[k])
+        u = U * 2.0 ** -53
+        assert round(math.pow(u, power) * mx) >= k + 1 > np.round(np.power(np.array([u]), float(power))[0] * mx)
+    assert np.count_nonzero(c != ref) <= 2
+    if (power, mx) in ((100, 200), (60, 200), (400, 200), (2.5, 7), (1, 255)):
+        assert np.array_equal(c, ref)
+
+
+def test_c_bush_thresholds_rejects_bad_arguments():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libwab_hip.so not built")
+    L = _lib.load()
+    assert L.wab_bush_thresholds(100.0, 256, None) == -1
+    assert L.wab_bush_thresholds(float("nan"), 10, None) == -1
+    assert L.wab_bush_thresholds(100.0, 10, None) == -1

@@ -225,33 +225,42 @@ def test_reset_mask_only_touches_masked_envs():
 
 
 def test_bad_action_raises_and_counts():
-    """Device actions out of range: step() does not synchronise; the kernel applies them as
-    no-ops and counts them, and the next synchronising call raises the IndexError (once).
-    Host actions and validate_actions="sync" raise in step() itself."""
+    """validate_actions=True (the default, "sync"): an out-of-range action raises IndexError
+    from step() itself, host or device.  "deferred": step() does not synchronise; the kernel
+    applies the actions as no-ops and counts them, and the next synchronising call (counters,
+    state, check, reset) raises once, with what it read attached as err.result."""
     import torch
 
     env = _env(None, 128)
     env.reset()
-    env.step(torch.full((128,), 5, device="cuda:0"))  # asynchronous
     with pytest.raises(IndexError):
+        env.step(torch.full((128,), 5, device="cuda:0"))   # device actions: immediate
+    with pytest.raises(IndexError):
+        env.step(np.full(128, 5))                          # host actions: before the copy
+    with pytest.raises(IndexError):
+        env.rollout(torch.full((2, 128), 5, device="cuda:0"))
+    env.validate_actions = "deferred"
+    env.step(torch.full((128,), 5, device="cuda:0"))  # asynchronous
+    with pytest.raises(IndexError) as ei:
         env.counters()
+    assert ei.value.result["bad_actions"] == 128
     env.check()  # reported once
     env.step(torch.full((128,), 2, device="cuda:0"))
     env.step(torch.full((128,), -3, device="cuda:0", dtype=torch.int8))
-    with pytest.raises(IndexError):
+    with pytest.raises(IndexError) as ei:
         env.state()
+    assert ei.value.result["turn"].shape == (128,)
+    env.step(torch.full((128,), 7, device="cuda:0"))
     with pytest.raises(IndexError):
-        env.step(np.full(128, 5))  # host actions: checked before the copy
-    env.validate_actions = "sync"
-    with pytest.raises(IndexError):
-        env.step(torch.full((128,), 5, device="cuda:0"))
+        env.reset()
+    env.reset()
     env.validate_actions = False
     env.step(torch.full((128,), -1))
     env.step(torch.full((128,), 261))  # int64 261 must not narrow to the valid action 5
     env.step(np.full(128, 256))        # nor 256 to 0
     c = env.counters()
-    assert c["bad_actions"] == 128 * 5
-    assert c["steps"] == 128 * 6 and c["handoff_timeouts"] == 0
+    assert c["bad_actions"] == 128 * 6
+    assert c["steps"] == 128 * 7 and c["handoff_timeouts"] == 0
 
 
 def test_input_shape_checks():

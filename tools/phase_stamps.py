@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--lib", default=OUT, help="the stamps library to load (with --no-build)")
     ap.add_argument("--b2b", type=int, default=0,
                     help="instead: per-XCD entry/end of the last two of N back-to-back launches")
+    ap.add_argument("--graph", action="store_true",
+                    help="with --b2b: the N launches captured in a graph and replayed (the bench's shape)")
     args = ap.parse_args()
     import __graft_entry__ as ge
 
@@ -56,7 +58,7 @@ def main():
     g.manual_seed(0)
     kind = env.step_kernel
     if args.b2b:
-        return b2b_report(env, L, g, args.steps, args.b2b)
+        return b2b_report(env, L, g, args.steps, args.b2b, args.graph)
     if kind == "small":
         return small_report(env, st, g, args.steps)
     if kind == "wide":
@@ -157,7 +159,7 @@ def wide_report(env, st, g, steps):
             name, us((s[idx, 10] - t0).mean()), us(obs[idx].mean()), us((s[idx, 14] - s[idx, 13]).mean()), us(e_[idx].mean())))
 
 
-def b2b_report(env, L, g, steps, n):
+def b2b_report(env, L, g, steps, n, graph=False):
     """Back-to-back launches as the bench issues them (no synchronisation in between): each
     launch stamps into one of two buffers, alternately; per XCD (the XCC_ID register) the mean
     kernel-entry offset of the last launch's workgroups from its first one, its mean and last
@@ -173,13 +175,31 @@ def b2b_report(env, L, g, steps, n):
     ends_cols = [6, 15, 21, 27] if env.step_kernel == "small" else [6, 14, 22, 30]
     acts = torch.randint(0, env.n_actions, (n, B), device="cuda:0", generator=g).to(torch.int8)
     entry, endx, lastx, gaps, spans, karg = [], [], [], [], [], []
+    gr = None
+    if graph:  # the stamp buffer pointer is a kernel argument: captured per launch
+        for i in range(n):  # warm
+            env.step(acts[i])
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(gr, stream=side):
+                for i in range(n):
+                    L.wab_debug_set_stamps(env._h, bufs[i % 2].data_ptr())
+                    env.step(acts[i])
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
     for t in range(steps):
         for b in bufs:
             b.zero_()
         torch.cuda.synchronize()
-        for i in range(n):
-            L.wab_debug_set_stamps(env._h, bufs[i % 2].data_ptr())
-            env.step(acts[i])
+        if gr is not None:
+            gr.replay()
+        else:
+            for i in range(n):
+                L.wab_debug_set_stamps(env._h, bufs[i % 2].data_ptr())
+                env.step(acts[i])
         torch.cuda.synchronize()
         last = bufs[(n - 1) % 2].cpu().numpy().astype(np.int64)[:nb]
         prev = bufs[(n - 2) % 2].cpu().numpy().astype(np.int64)[:nb]
@@ -194,7 +214,7 @@ def b2b_report(env, L, g, steps, n):
             karg.append([(last[xc == x, 34] - last[xc == x, 32]).mean() for x in range(8)])
         spans.append(end.max())
     us = lambda v: np.round(np.mean(v, axis=0) * 10 / 1000, 2)
-    print("back-to-back launches: %d x %d, last two stamped" % (steps, n))
+    print("back-to-back launches: %d x %d, last two stamped%s" % (steps, n, " (graph replay)" if graph else ""))
     print("entry by XCC, mean (us):   ", us(entry))
     print("end by XCC, mean (us):     ", us(endx))
     print("end by XCC, last (us):     ", us(lastx))

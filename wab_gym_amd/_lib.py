@@ -18,6 +18,7 @@ EXPORTED = [
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
     "wab_debug_bush_values", "wab_step_features", "wab_discounted_returns_exact",
+    "wab_bush_thresholds",
 ]
 
 ABI_VERSION = 2
@@ -76,6 +77,7 @@ def load():
     L.wab_debug_bush_values.argtypes = [P, P, P, I64, P]
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_discounted_returns_exact.argtypes = [P, P, P, I32, I64, ctypes.c_double, P, P, P]
+    L.wab_bush_thresholds.argtypes = [ctypes.c_double, I32, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64
     L.wab_step_kernel.argtypes = [P]

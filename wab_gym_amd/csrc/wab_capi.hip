@@ -30,8 +30,10 @@ __global__ void wab_featurize_kernel(FeatParams p);
 __global__ void wab_featurize_small_kernel(FeatParams p);
 __global__ void wab_render_kernel(RenderParams p);
 __global__ void wab_egocentric_kernel(EgoParams p);
-__global__ void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T, int64_t B,
-                                   double gamma, const float* bootstrap, float* out, RewardTable tab);
+template <int VEC>
+__global__ void wab_returns_kernel(const float* __restrict__ reward, const uint8_t* __restrict__ done, int32_t T,
+                                   int64_t B, double gamma, const float* __restrict__ bootstrap,
+                                   float* __restrict__ out, RewardTable tab);
 }
 
 using wab::Params;
@@ -242,6 +244,24 @@ bool feat_small_ok(const Params& p) {
   return p.W * p.H <= 128 && p.S == p.H && max_dist < md;
 }
 
+// the discounted-return scan: four envs per thread when every [t] row is 16-byte aligned (B a
+// multiple of 4, aligned base pointers), else one
+int launch_returns(const float* reward, const uint8_t* done, int32_t T, int64_t B, double gamma,
+                   const float* bootstrap, float* returns, const wab::RewardTable& tab, void* stream) {
+  const bool vec4 = B % 4 == 0 && aligned16(reward) && aligned16(returns) && ((uintptr_t)done & 3u) == 0 &&
+                    ((uintptr_t)bootstrap & 3u) == 0;
+  const int64_t threads = vec4 ? B / 4 : B;
+  const dim3 grid((unsigned)((threads + 63) / 64));
+  if (vec4)
+    hipLaunchKernelGGL(wab::wab_returns_kernel<4>, grid, dim3(64), 0, (hipStream_t)stream, reward, done, T, B,
+                       gamma, bootstrap, returns, tab);
+  else
+    hipLaunchKernelGGL(wab::wab_returns_kernel<1>, grid, dim3(64), 0, (hipStream_t)stream, reward, done, T, B,
+                       gamma, bootstrap, returns, tab);
+  HIP_TRY(hipGetLastError());
+  return WAB_OK;
+}
+
 int check_obs(const wab_obs* o, const char* what) {
   if (!o || !o->planes || !o->food_turns || !o->role || !o->status)
     return fail(WAB_E_INVALID, std::string(what) + ": every wab_obs pointer must be set");
@@ -258,6 +278,33 @@ int wab_abi_version(void) { return WAB_ABI_VERSION; }
 const char* wab_last_error(void) { return g_err.c_str(); }
 
 int wab_num_actions(const wab_config* cfg) { return cfg ? n_actions_of(cfg) : WAB_E_INVALID; }
+
+// generate_n_bush_values (wab_env.py:631-635): value(U) = round_half_even((U 2^-53) ** power * max).
+// For each k the smallest U on the 2^53 grid with value >= k, by bisection (the value is
+// monotone in U), evaluated with libm pow and rint in the reference's operation order.
+int wab_bush_thresholds(double bush_power, int32_t max_berries, uint64_t* out) {
+  g_err.clear();
+  if (max_berries < 0 || max_berries > 255) return fail(WAB_E_INVALID, "max_berries_per_bush must be in [0, 255]");
+  if (!(bush_power >= 0.0) || !std::isfinite(bush_power))
+    return fail(WAB_E_INVALID, "bush_power must be a finite number >= 0");
+  if (max_berries > 0 && !out) return fail(WAB_E_INVALID, "wab_bush_thresholds: NULL out");
+  const double mx = (double)max_berries;
+  auto value = [&](int64_t U) {
+    volatile double u = (double)U * 0x1p-53;  // exact: U < 2^53
+    volatile double pw = std::pow((double)u, bush_power);
+    volatile double scaled = pw * mx;
+    return std::nearbyint((double)scaled);  // default rounding: half to even, as np.round
+  };
+  for (int k = 1; k <= max_berries; ++k) {
+    int64_t lo = 0, hi = (int64_t)1 << 53;  // value(lo) < k (taken, as by options.py), value(hi) >= k; 2^53 = "never"
+    while (hi - lo > 1) {
+      const int64_t mid = lo + (hi - lo) / 2;
+      if (value(mid) >= (double)k) hi = mid; else lo = mid;
+    }
+    out[k - 1] = (uint64_t)hi;
+  }
+  return WAB_OK;
+}
 
 int64_t wab_batch(const wab_handle* h) { return h ? h->p.B : 0; }
 
@@ -280,8 +327,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     return fail(WAB_E_INVALID, "restrict_view needs width, height >= 11 (11x11 masks, wab_env.py:354)");
   if (c->max_berries_per_bush < 0 || c->max_berries_per_bush > 255)
     return fail(WAB_E_INVALID, "max_berries_per_bush must be in [0, 255]");
-  if (c->max_berries_per_bush > 0 && !c->bush_thresholds)
-    return fail(WAB_E_INVALID, "bush_thresholds is required");
+  if (!(c->bush_power >= 0.0) || !std::isfinite(c->bush_power))
+    return fail(WAB_E_INVALID, "bush_power must be a finite number >= 0");
   if (c->turns_to_fill_food <= 0 || c->turns_to_empty_food <= 0)
     return fail(WAB_E_INVALID, "turns_to_fill_food / turns_to_empty_food must be > 0");
   if (c->turns_to_empty_food > 255) return fail(WAB_E_INVALID, "turns_to_empty_food must be <= 255 (u8 obs)");
@@ -325,7 +372,15 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   const uint64_t spawn_ge = (uint64_t)std::ceil(std::ldexp(c->chance_wolf_on_square / 2.0, 53));  // u < p/2 (:573)
   p.max_berries = c->max_berries_per_bush;
   p.bush_power = (float)c->bush_power;
-  const uint64_t bush_ge = p.max_berries > 0 ? c->bush_thresholds[0] : (1ull << 53);          // food > 0
+  // the caller's table (the Python host computes it with numpy), or the same table from libm
+  std::vector<uint64_t> thr_own;
+  const uint64_t* thr_host = c->bush_thresholds;
+  if (p.max_berries > 0 && !thr_host) {
+    thr_own.resize((size_t)p.max_berries);
+    wab_bush_thresholds(c->bush_power, p.max_berries, thr_own.data());
+    thr_host = thr_own.data();
+  }
+  const uint64_t bush_ge = p.max_berries > 0 ? thr_host[0] : (1ull << 53);          // food > 0
   split_threshold(keep_ge, &p.keep_th, &p.keep_tl);
   split_threshold(bush_ge, &p.bush_th, &p.bush_tl);
   // keyed spawn sets (oracle/keyed_rng.py gap_thresholds): gap[g] = floor((1 - q)^g 2^53),
@@ -485,7 +540,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   }
   if (e == hipSuccess) e = hipMemcpy(gap, gap_host.data(), gap_host.size() * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess && p.max_berries > 0)
-    e = hipMemcpy(thr, c->bush_thresholds, (size_t)p.max_berries * 8, hipMemcpyHostToDevice);
+    e = hipMemcpy(thr, thr_host, (size_t)p.max_berries * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess && B > 0) {  // every env: episode 0xFFFFFFFF (the first reset makes it 0)
     std::vector<uint4> init(B, make_uint4(0u, 0u, 0u, 0xFFFFFFFFu));
     e = hipMemcpy(p.hdr, init.data(), B * 16, hipMemcpyHostToDevice);
@@ -869,10 +924,7 @@ int wab_discounted_returns(const float* reward, const uint8_t* done, int32_t T, 
   if (T == 0 || B == 0) return WAB_OK;
   wab::RewardTable none;
   std::memset(&none, 0, sizeof(none));
-  hipLaunchKernelGGL(wab::wab_returns_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns, none);
-  HIP_TRY(hipGetLastError());
-  return WAB_OK;
+  return launch_returns(reward, done, T, B, gamma, bootstrap, returns, none, stream);
 }
 
 int wab_discounted_returns_exact(const wab_handle* h, const float* reward, const uint8_t* done, int32_t T,
@@ -885,10 +937,7 @@ int wab_discounted_returns_exact(const wab_handle* h, const float* reward, const
                                "float32; the double rewards are not recoverable");
   if (T == 0 || B == 0) return WAB_OK;
   DeviceGuard guard(h->device);
-  hipLaunchKernelGGL(wab::wab_returns_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, reward, done, T, B, gamma, bootstrap, returns, h->rewards);
-  HIP_TRY(hipGetLastError());
-  return WAB_OK;
+  return launch_returns(reward, done, T, B, gamma, bootstrap, returns, h->rewards, stream);
 }
 
 int wab_debug_bush_values(wab_handle* h, const uint64_t* U, int32_t* out, int64_t n, void* stream) {

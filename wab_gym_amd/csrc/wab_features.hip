@@ -294,25 +294,74 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
     store_feature_bits(ob, p.out + (size_t)g0 * p.F, (uint32_t)n_active * (uint32_t)p.F, tid, 256);
 }
 
-// actor_critic.finish_episode returns (actor_critic.py:139-143), one thread per env
-__global__ __launch_bounds__(256) void wab_returns_kernel(const float* reward, const uint8_t* done, int32_t T,
-                                                          int64_t B, double gamma, const float* bootstrap,
-                                                          float* out, RewardTable tab) {
-  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// actor_critic.finish_episode returns (actor_critic.py:139-143): R_t = r_t + gamma R_{t+1},
+// restarted after every done_t.  The scan is a serial chain in t, so each thread first issues
+// the loads of a whole chunk of kReturnsChunk steps (registers), then runs the chain; VEC
+// consecutive envs per thread (VEC = 4: one 16-byte reward and one 4-byte done load per step,
+// four independent chains).  64-thread workgroups: B = 65536 is 256 (VEC 4) or 1024 (VEC 1)
+// workgroups, so every CU holds a wave.  Double accumulation (the reference's Python floats),
+// no contraction (-ffp-contract=off), float32 out.
+constexpr int kReturnsChunk = 32;
+
+template <int VEC>
+__global__ __launch_bounds__(64) void wab_returns_kernel(const float* __restrict__ reward,
+                                                         const uint8_t* __restrict__ done, int32_t T, int64_t B,
+                                                         double gamma, const float* __restrict__ bootstrap,
+                                                         float* __restrict__ out, RewardTable tab) {
+  const int64_t b = ((int64_t)blockIdx.x * 64 + threadIdx.x) * VEC;
   if (b >= B) return;
-  double R = bootstrap ? (double)bootstrap[b] : 0.0;
-  for (int32_t t = T - 1; t >= 0; --t) {
-    const int64_t i = (int64_t)t * B + b;
-    if (done[i]) R = 0.0;
-    // the step's exact double reward when the table has it (the env's own rewards), else the
-    // float32 as given
-    const float rf = reward[i];
-    double r = (double)rf;
-    for (int k = 0; k < tab.n; ++k)
-      if (__float_as_uint(rf) == tab.f32[k]) r = tab.f64[k];
-    R = r + gamma * R;  // (no contraction: -ffp-contract=off, the reference's op order)
-    out[i] = (float)R;
+  double R[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) R[v] = bootstrap ? (double)bootstrap[b + v] : 0.0;
+  for (int32_t hi = T - 1; hi >= 0; hi -= kReturnsChunk) {
+    const int n = hi + 1 < kReturnsChunk ? hi + 1 : kReturnsChunk;  // steps hi, hi-1, .., hi-n+1
+    float rf[kReturnsChunk][VEC];
+    uint32_t dn[kReturnsChunk];
+#pragma unroll
+    for (int j = 0; j < kReturnsChunk; ++j) {
+      if (j < n) {
+        const int64_t i = (int64_t)(hi - j) * B + b;
+        if constexpr (VEC == 4) {
+          const float4 r4 = *reinterpret_cast<const float4*>(reward + i);
+          rf[j][0] = r4.x; rf[j][1] = r4.y; rf[j][2] = r4.z; rf[j][3] = r4.w;
+          dn[j] = *reinterpret_cast<const uint32_t*>(done + i);
+        } else {
+          rf[j][0] = reward[i];
+          dn[j] = done[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kReturnsChunk; ++j) {
+      if (j < n) {
+        float o[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          if ((dn[j] >> (8 * v)) & 0xFFu) R[v] = 0.0;
+          // the step's exact double reward when the table has it (the env's own rewards),
+          // else the float32 as given
+          double r = (double)rf[j][v];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k < tab.n && __float_as_uint(rf[j][v]) == tab.f32[k]) r = tab.f64[k];
+          R[v] = r + gamma * R[v];
+          o[v] = (float)R[v];
+        }
+        const int64_t i = (int64_t)(hi - j) * B + b;
+        if constexpr (VEC == 4)
+          *reinterpret_cast<float4*>(out + i) = make_float4(o[0], o[1], o[2], o[3]);
+        else
+          out[i] = o[0];
+      }
+    }
   }
 }
+
+template __global__ void wab_returns_kernel<1>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+                                               int64_t, double, const float* __restrict__, float* __restrict__,
+                                               RewardTable);
+template __global__ void wab_returns_kernel<4>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+                                               int64_t, double, const float* __restrict__, float* __restrict__,
+                                               RewardTable);
 
 }  // namespace wab

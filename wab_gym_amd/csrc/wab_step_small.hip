@@ -389,14 +389,27 @@ __device__ __forceinline__ void store_unit(uint8_t* out, const uint32_t* stream,
   __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
 }
 
-// units [64 k + lane] for k = first, first + stride, ... that touch a done env iff `touching`
+// units [64 k + lane] for k = first, first + stride, ... whose 128-byte line (absolute
+// address) holds a byte of a done env iff `touching` (WAB_EARLY_LINES=1; else the unit's own
+// 16 bytes decide).  A line is then written in one phase: a line written in parts at two
+// times is a partial-line write to HBM.
+#ifndef WAB_EARLY_LINES
+#define WAB_EARLY_LINES 1
+#endif
 __device__ __forceinline__ void store_units(const Params& p, const uint32_t* stream, unsigned long long jm,
                                             bool touching, int first, int stride, int lane) {
   const uint32_t OB = (uint32_t)p.OB, full = (64u * OB) >> 4;
   uint8_t* out = p.planes + (size_t)blockIdx.x * 64u * OB;
+  const uint32_t mis = (uint32_t)reinterpret_cast<uintptr_t>(out) & 127u;  // group start within its line
   for (uint32_t u = 64u * (uint32_t)first + (uint32_t)lane; u < full; u += 64u * (uint32_t)stride) {
-    const uint32_t e0 = (16u * u) / OB, e1 = (16u * u + 15u) / OB;
-    const bool t = (((jm >> e0) | (jm >> e1)) & 1ull) != 0ull;
+    uint32_t b0 = 16u * u, b1 = 16u * u + 15u;
+    if (WAB_EARLY_LINES) {  // the line's bytes within the group
+      const uint32_t l0 = (b0 + mis) & ~127u;
+      b0 = l0 > mis ? l0 - mis : 0u;
+      b1 = min(l0 + 127u - mis, 64u * OB - 1u);
+    }
+    const uint32_t e0 = b0 / OB, e1 = b1 / OB;  // (a line may span more than two envs when OB < 128)
+    const bool t = ((jm >> e0) & ((2ull << (e1 - e0)) - 1ull)) != 0ull;
     if (t == touching) store_unit(out, stream, u);
   }
 }

@@ -17,12 +17,17 @@ Differences from the reference, by design (documented in DESIGN.md):
   * with `autoreset=True` (default) an env whose step returns done=True is reset inside
     the same call; `obs` then holds the new episode's first observation and
     `info["terminal_obs"]` (if `return_terminal=True`) the step's own observation;
-  * an action outside [0, n_actions) raises IndexError (the reference raises for
-    a >= n via `.iloc` and silently wraps negatives, wab_env.py:253).  Host actions are
-    checked before their copy; device actions are checked by the kernel (the step applies
-    them as no-ops and counts them) and the IndexError is raised by the next synchronising
-    call -- counters(), state() or check() -- so step() never waits for the device
-    (validate_actions="sync" restores an immediate, synchronising check).
+  * an action outside [0, n_actions) raises IndexError from the call that received it
+    (the reference raises for a >= n via `.iloc` and silently wraps negatives,
+    wab_env.py:253).  Host actions are checked before their copy; device actions with one
+    synchronising reduction per call (validate_actions=True, the default, = "sync").
+    validate_actions="deferred" (opt-in, for throughput) skips that synchronisation: the
+    kernel applies out-of-range actions as no-ops and counts them, and the IndexError comes
+    from the next synchronising call -- counters(), state(), check() -- or the next reset();
+    the data that call read is attached to the exception (`err.result`).
+  * the kernel's LDS hand-off between its waves is bounded (wab_device.h lds_await); a
+    timed-out hand-off means results computed from unpublished data, so a non-zero
+    `handoff_timeouts` count raises WabError from counters(), state() and check().
 """
 from __future__ import annotations
 
@@ -57,9 +62,10 @@ class BatchedWolvesAndBushesEnv:
         self.autoreset = bool(autoreset)
         self.return_terminal = bool(return_terminal)
         if validate_actions not in (True, False, "sync", "deferred"):
-            raise ValueError("validate_actions must be True/'deferred', 'sync' or False")
-        self.validate_actions = validate_actions
+            raise ValueError("validate_actions must be True/'sync', 'deferred' or False")
+        self.validate_actions = "sync" if validate_actions is True else validate_actions
         self._bad_seen = 0  # bad_actions already reported (deferred validation)
+        self._handoff_seen = 0  # handoff_timeouts already reported
         dev = torch.device(device)
         if dev.type != "cuda":
             raise ValueError("BatchedWolvesAndBushesEnv runs on a HIP device (device='cuda[:i]')")
@@ -103,6 +109,22 @@ class BatchedWolvesAndBushesEnv:
         st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr())
         return {"planes": planes, "scalars": scal, "struct": st}
 
+    def _obs_struct(self, obs):
+        """WabObs over a caller's observation dict (planes [B,3,W,S] and scalars [3,B] u8 on
+        this env's device), checked before any pointer reaches a kernel: a wrong dtype,
+        device or batch would be an out-of-bounds device read.  Returns (struct, keepalive)."""
+        t = self._torch
+        planes, scal = obs["planes"], obs["scalars"]
+        want = (self.num_envs, 3, self.W, self.S)
+        for name, x, shape in (("planes", planes, want), ("scalars", scal, (3, self.num_envs))):
+            if (not isinstance(x, t.Tensor) or x.dtype != t.uint8 or x.device != self.device
+                    or tuple(x.shape) != shape):
+                raise ValueError("obs['%s'] must be a uint8 tensor of shape %s on %s"
+                                 % (name, shape, self.device))
+        planes, scal = planes.contiguous(), scal.contiguous()
+        st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr())
+        return st, (planes, scal)
+
     def _obs_tuple(self, o):
         planes, scal = o["planes"], o["scalars"]
         H = self.H
@@ -121,6 +143,9 @@ class BatchedWolvesAndBushesEnv:
         """Reset all envs (mask=None) or those with mask[i] true; returns the batched obs."""
         t = self._torch
         m = None
+        if self.validate_actions == "deferred" and self._reset_once:
+            # a deferred out-of-range action must not disappear behind the new episodes
+            self._raise_pending(self._read_counters(), None)
         if mask is not None:
             if not self._reset_once:
                 raise RuntimeError("the first reset must cover every env (mask=None)")
@@ -154,11 +179,10 @@ class BatchedWolvesAndBushesEnv:
             a = actions.to(self.device)
             if a.shape != (self.num_envs,):
                 raise ValueError("actions must have shape [num_envs]")
-            # device actions: the kernel counts out-of-range actions (applied as no-ops);
-            # validate_actions=True raises at the next synchronising call, "sync" here
-            # (one blocking reduction per step)
-            if self.validate_actions == "sync" and bool(((a < 0) | (a >= self.n_actions)).any()):
-                raise IndexError("action out of range [0, %d)" % self.n_actions)
+            # device actions: "sync" (the default) checks here with one blocking reduction
+            # per step; "deferred" lets the kernel count them (applied as no-ops) and raises
+            # at the next synchronising call
+            self._sync_action_check(a)
         if a.dtype != t.int8:
             # narrowing must not wrap an out-of-range value into a valid one (256 -> 0)
             self._actions.copy_(a.clamp(-1, 127) if not a.is_floating_point() else a.clamp(-1.0, 127.0))
@@ -174,17 +198,38 @@ class BatchedWolvesAndBushesEnv:
             raise ValueError("features must be a contiguous float32 tensor of shape (%d, %d) on %s"
                              % (self.num_envs, F, self.device))
 
-    def _deferred_action_check(self, bad_actions):
-        """Raise the IndexError of out-of-range device actions stepped since the last check
-        (validate_actions=True): they were applied as no-ops, counted by the kernel."""
-        new = bad_actions - self._bad_seen
-        self._bad_seen = bad_actions
-        if self.validate_actions and new > 0:
-            raise IndexError("%d action(s) out of range [0, %d) were stepped since the last check "
-                             "(applied as no-ops)" % (new, self.n_actions))
+    def _sync_action_check(self, a):
+        if self.validate_actions == "sync" and a.numel() and bool(((a < 0) | (a >= self.n_actions)).any()):
+            raise IndexError("action out of range [0, %d)" % self.n_actions)
+
+    def _raise_pending(self, c, result):
+        """Raise what the device counters report since the last check: a WabError for
+        timed-out LDS hand-offs (the step then computed from unpublished data), an IndexError
+        for out-of-range device actions stepped under validate_actions="deferred" (applied as
+        no-ops).  `result` (the data the calling method read) rides on the exception."""
+        hand = c["handoff_timeouts"] - self._handoff_seen
+        self._handoff_seen = c["handoff_timeouts"]
+        bad = c["bad_actions"] - self._bad_seen
+        self._bad_seen = c["bad_actions"]
+        err = None
+        if hand > 0:
+            err = _lib.WabError("%d LDS hand-off(s) timed out in the step kernel since the last check: "
+                                "the affected steps are not reference results" % hand)
+        elif self.validate_actions and bad > 0:
+            err = IndexError("%d action(s) out of range [0, %d) were stepped since the last check "
+                             "(applied as no-ops)" % (bad, self.n_actions))
+        if err is not None:
+            err.result = result
+            raise err
+
+    def _read_counters(self):
+        c = _lib.WabCounters()
+        _lib.check(_lib.load().wab_get_counters(self._h, ctypes.addressof(c), self._stream()),
+                   "wab_get_counters")
+        return {k: int(getattr(c, k)) for k, _ in _lib.WabCounters._fields_}
 
     def check(self):
-        """Synchronise and raise the deferred IndexError of out-of-range device actions."""
+        """Synchronise; raise for timed-out hand-offs and deferred out-of-range actions."""
         self.counters()
 
     def step(self, actions):
@@ -222,6 +267,7 @@ class BatchedWolvesAndBushesEnv:
         a = t.as_tensor(actions, device=self.device)
         if a.dim() != 2 or a.shape[1] != self.num_envs:
             raise ValueError("actions must have shape [T, num_envs]")
+        self._sync_action_check(a)
         if a.dtype != t.int8:
             a = a.clamp(-1, 127)
         a = a.to(t.int8).contiguous()
@@ -253,9 +299,7 @@ class BatchedWolvesAndBushesEnv:
         if obs is None:
             st = self._obs["struct"]
         else:
-            planes, scal = obs["planes"].contiguous(), obs["scalars"].contiguous()
-            st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr())
-            keep = (planes, scal)
+            st, keep = self._obs_struct(obs)
         _lib.check(_lib.load().wab_render(self._h, ctypes.addressof(st), int(scale), int(bool(draw_health)),
                                           img.data_ptr(), self._stream()), "wab_render")
         del keep
@@ -267,11 +311,11 @@ class BatchedWolvesAndBushesEnv:
         return _lib.load().wab_step_kernel(self._h).decode()
 
     def counters(self):
-        c = _lib.WabCounters()
-        _lib.check(_lib.load().wab_get_counters(self._h, ctypes.addressof(c), self._stream()),
-                   "wab_get_counters")
-        out = {k: int(getattr(c, k)) for k, _ in _lib.WabCounters._fields_}
-        self._deferred_action_check(out["bad_actions"])
+        """The handle's cumulative counters (wab_counters).  Raises (counters attached as
+        `err.result`) for hand-off timeouts and deferred out-of-range actions since the last
+        check."""
+        out = self._read_counters()
+        self._raise_pending(out, out)
         return out
 
     def state(self):
@@ -283,9 +327,9 @@ class BatchedWolvesAndBushesEnv:
         P = lambda a: a.ctypes.data  # noqa: E731
         _lib.check(_lib.load().wab_get_state(self._h, P(food), P(x), P(y), P(turn), P(nw), P(ep),
                                              self._stream()), "wab_get_state")
-        if self.validate_actions:
-            self.counters()  # (raises the deferred IndexError, if any)
-        return dict(food=food, x=x, y=y, turn=turn, n_wolves=nw, episode=ep)
+        out = dict(food=food, x=x, y=y, turn=turn, n_wolves=nw, episode=ep)
+        self._raise_pending(self._read_counters(), out)
+        return out
 
     def seed(self, seed=None):
         """No-op like gym 0.17's Env.seed in the reference (wab_env.py:1014); draws are keyed

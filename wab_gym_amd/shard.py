@@ -9,6 +9,62 @@ per-rank figures (bench.py).  RCCL is never initialised.
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import threading
+import time
+
+
+def free_port(host="127.0.0.1") -> int:
+    """An unused TCP port on `host` for the rendezvous."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(cmd, n, env=None, master_port=None, timeout=None):
+    """Run `cmd` (an argv list) as `n` fresh rank processes, one per GPU, the way
+    `torch.distributed.run --nproc-per-node n --master-addr 127.0.0.1` would: child r gets
+    RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n and MASTER_ADDR/PORT.  The caller
+    must not have touched the GPU (the children are started, not exec'd).  Returns
+    (exit code, rank 0's stdout, every rank's exit code): the exit code is that of the first
+    child to fail on its own (lowest rank among simultaneous failures; 0 when all succeed).
+    If one child fails the rest are killed, so a rank stuck at a barrier cannot hang the
+    launch; on `timeout` (seconds) every child still running is killed and the code is -9."""
+    base = dict(os.environ if env is None else env)
+    port = master_port or free_port()
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # rank 0's stdout is captured (it carries the JSON line); the others inherit ours
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else None))
+    out0 = []
+
+    def pump():
+        for line in procs[0].stdout:
+            out0.append(line.decode(errors="replace"))
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    codes = [None] * n
+    t_end = None if timeout is None else time.monotonic() + timeout
+    first_failure = 0
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        failed = [c for c in codes if c not in (None, 0)]
+        late = t_end is not None and time.monotonic() > t_end
+        if failed or late:
+            first_failure = failed[0] if failed else -9
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    p.kill()
+                    codes[r] = p.wait() or -9
+            break
+        time.sleep(0.05)
+    th.join(timeout=10)
+    return first_failure, "".join(out0), codes
 
 
 def rank_info():

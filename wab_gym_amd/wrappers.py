@@ -10,6 +10,7 @@ float32 tensor [B, 449] computed on device by one HIP kernel (wab_featurize).
 from __future__ import annotations
 
 import ctypes
+import warnings
 
 from . import _lib
 from .spaces import Box, Discrete, Tuple
@@ -51,11 +52,7 @@ class PragmaticObsWrapper:
             st = env._obs["struct"]
             keep = None
         else:
-            planes = obs["planes"].contiguous()
-            scal = obs["scalars"].contiguous()
-            st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(),
-                             scal[2].data_ptr())
-            keep = (planes, scal)
+            st, keep = env._obs_struct(obs)
         vm = None
         if view_mask is not None:
             vm = t.as_tensor(view_mask, device=env.device).to(t.uint8).contiguous()
@@ -112,11 +109,7 @@ class SuperBasicObservationWrapper(PragmaticObsWrapper):
             st = env._obs["struct"]
             keep = None
         else:
-            planes = obs["planes"].contiguous()
-            scal = obs["scalars"].contiguous()
-            st = _lib.WabObs(planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(),
-                             scal[2].data_ptr())
-            keep = (planes, scal)
+            st, keep = env._obs_struct(obs)
         dst = self.features if out is None else out
         env._check_features(dst, self.feature_dim)
         _lib.check(_lib.load().wab_featurize_superbasic(env._h, ctypes.addressof(st), dst.data_ptr(),
@@ -146,10 +139,18 @@ def discounted_returns(reward, done, gamma=0.99, bootstrap=None, out=None, env=N
     L = _lib.load()
     args = (r.data_ptr(), d.data_ptr(), T, B, float(gamma), None if bs is None else bs.data_ptr(), o.data_ptr(),
             stream)
-    if env is None:
-        _lib.check(L.wab_discounted_returns(*args), "wab_discounted_returns")
-    else:
-        _lib.check(L.wab_discounted_returns_exact(env._h, *args), "wab_discounted_returns_exact")
+    if env is not None:
+        if r.device != env.device:
+            raise ValueError("reward is on %s, the env on %s" % (r.device, env.device))
+        try:
+            _lib.check(L.wab_discounted_returns_exact(env._h, *args), "wab_discounted_returns_exact")
+            return o
+        except ValueError as e:
+            if "round to the same" not in str(e):
+                raise
+            # two of the options' rewards are one float32: the doubles are not recoverable
+            warnings.warn("discounted_returns(env=...): %s; using the float32 rewards" % e)
+    _lib.check(L.wab_discounted_returns(*args), "wab_discounted_returns")
     return o
 
 
