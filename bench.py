@@ -34,8 +34,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 CONFIGS = {
     # name: (game options, plane_stride, wolf slots, description)
     "default": ({}, 0, 8, "batch=65536 envs x default options (11x11 viewport), random policy, autoreset"),
-    # 16 wolf slots: with 8, a 961-cell reset view overflows a few times per million resets
-    "wide31": ({"width": 31, "height": 31}, 32, 16,
+    # "8 wolves" (SURVEY.md A.5): the wide kernel keeps 8 wolves per env in registers; the
+    # handle's 32 wolf rows let the rare 9th+ (ring spawns mid-episode: 14 in a 2000-step window
+    # at 8 rows) live in HBM instead of being dropped
+    "wide31": ({"width": 31, "height": 31}, 32, 32,
                "batch=65536 envs x 31x31 viewport in 32x32 planes (C3), random policy, autoreset"),
     # C5: per step the step fused with the PragmaticObsWrapper features (wab_step_features) into
     # a [T, B, 449] rollout buffer, reward/done straight into [T, B]; every T steps the
@@ -201,7 +203,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
-                    help="override the config's wolf slot capacity (0: the config's own)")
+                    help="override the config's wolf rows per env (0: the config's own; the wide "
+                         "kernel keeps 8 of them in registers)")
     ap.add_argument("--c5-unfused", action="store_true",
                     help="C5 as wab_step + wab_featurize (obs planes stored) instead of wab_step_features")
     args = ap.parse_args()
@@ -456,7 +459,8 @@ def main():
             "warmup_requested": args.warmup,
             "warmup_effective": W,
             "timed_window": window,
-            "overflow": {"wolf": counters["wolf_overflow"], "eaten": counters["eaten_overflow"],
+            "overflow": {"wolf": counters["wolf_overflow"], "wolf_at_reset": counters["wolf_overflow_reset"],
+                         "eaten": counters["eaten_overflow"],
                          "handoff_timeouts": counters["handoff_timeouts"]},
         }
         valu = committed_pmc(args.config, B) if not args.c5_unfused else None

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define WAB_ABI_VERSION 2
+#define WAB_ABI_VERSION 3
 #define WAB_MAX_WOLF_SLOTS 32 /* largest per-env live-wolf slot count (wab_config.wolf_slots) */
 #define WAB_MAX_VIEW 63       /* largest odd width/height accepted */
 
@@ -125,6 +125,8 @@ typedef struct wab_counters {
   uint64_t ego_missing;      /* wab_egocentric calls that found a turn of the path unrecorded */
   uint64_t handoff_timeouts; /* waits on an in-workgroup LDS hand-off that gave up (a hang
                               * guard; nonzero means results are invalid; must stay 0) */
+  uint64_t wolf_overflow_reset; /* the part of wolf_overflow dropped by resets (a new episode's
+                                 * initial wolves beyond the slots); the rest are ring spawns */
 } wab_counters;
 
 typedef struct wab_handle wab_handle;

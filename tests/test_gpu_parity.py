@@ -90,9 +90,10 @@ def test_c2_batch4096_default_lockstep():
 
 @pytest.mark.parametrize("return_terminal", [False, True])
 def test_c3_batch65536_wide31_padded_lockstep(return_terminal):
-    """C3 at full size with the bench's 16 wolf slots, past the turn-40 starvation (the first
-    mass auto-reset) to desynchronised second episodes."""
-    _lockstep({"width": 31, "height": 31}, 65536, 100, stride=32, wolf_slots=16,
+    """C3 at full size as the bench runs it (8 wolves per env in registers, 32 wolf rows: the
+    rare 9th+ in HBM), past the turn-40 starvation (the first mass auto-reset) to
+    desynchronised second episodes."""
+    _lockstep({"width": 31, "height": 31}, 65536, 100, stride=32, wolf_slots=32,
               return_terminal=return_terminal, seed_actions=3)
 
 

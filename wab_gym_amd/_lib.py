@@ -21,7 +21,7 @@ EXPORTED = [
     "wab_bush_thresholds",
 ]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class WabObs(ctypes.Structure):
@@ -33,7 +33,7 @@ class WabCounters(ctypes.Structure):
     _fields_ = [("wolf_overflow", ctypes.c_uint64), ("eaten_overflow", ctypes.c_uint64),
                 ("bad_actions", ctypes.c_uint64), ("steps", ctypes.c_uint64),
                 ("resets", ctypes.c_uint64), ("ego_missing", ctypes.c_uint64),
-                ("handoff_timeouts", ctypes.c_uint64)]
+                ("handoff_timeouts", ctypes.c_uint64), ("wolf_overflow_reset", ctypes.c_uint64)]
 
 
 class WabError(RuntimeError):

@@ -150,13 +150,12 @@ bool wide_view(const Params& p) {
          !p.restrict_view && wab::wide_layout(p).total * 4u <= 64u * 1024u;
 }
 
+// the wide kernel holds kWideRegSlots wolves per env in registers whatever wolf_slots is; a lane
+// with more works on the rest (rows kWideRegSlots..wolf_slots-1) from HBM (a rare path)
+constexpr int kWideRegSlots = 8;
 template <int MODE>
-void* wide_kernel_ptr(int slots) {
-  switch (slots) {
-    case 8: return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, 8>);
-    case 16: return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, 16>);
-    default: return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, 32>);
-  }
+void* wide_kernel_ptr(int) {
+  return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, kWideRegSlots>);
 }
 
 template <int G>
@@ -185,11 +184,7 @@ int launch(wab_handle* h, const Params& p, hipStream_t stream) {
   if (h->step_kernel == KERNEL_WIDE) {
     const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
     const size_t lds = h->wide_lds_bytes;
-    switch (h->slots) {
-      case 8: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 8>), grid, block, lds, stream, p); break;
-      case 16: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 16>), grid, block, lds, stream, p); break;
-      default: hipLaunchKernelGGL((wab::wab_step_wide<MODE, 32>), grid, block, lds, stream, p); break;
-    }
+    hipLaunchKernelGGL((wab::wab_step_wide<MODE, kWideRegSlots>), grid, block, lds, stream, p);
   } else if (MODE == 0 && h->step_kernel == KERNEL_SMALL) {
     if (h->small_g11) launch_small<11>(h, p, stream);
     else launch_small<0>(h, p, stream);
@@ -462,6 +457,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   p.eaten_cap = cap;
   h->device = device;
   h->slots = slots;
+  p.wolf_cap = slots;
   h->n_blocks = (int)((batch + wab::kEnvsPerBlock - 1) / wab::kEnvsPerBlock);
   h->lds_bytes = (size_t)wab::lds_layout(p, slots).total * 4u;
   {
@@ -681,6 +677,7 @@ int wab_get_counters(wab_handle* h, wab_counters* out, void* stream) {
   out->ego_missing = c[wab::CTR_EGO_MISSING];
   out->steps = c[wab::CTR_STEPS];
   out->handoff_timeouts = c[wab::CTR_HANDOFF_TIMEOUTS];
+  out->wolf_overflow_reset = c[wab::CTR_WOLF_OVERFLOW_RESET];
   out->resets = 0;
   for (size_t i = 0; i < br.size(); ++i) out->resets += br[i];
   return WAB_OK;

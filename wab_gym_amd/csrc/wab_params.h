@@ -21,6 +21,7 @@ enum : int {
   CTR_EGO_MISSING = 3,
   CTR_STEPS = 4,             // + B per step launch (one lane of workgroup 0)
   CTR_HANDOFF_TIMEOUTS = 5,  // bounded LDS hand-off waits that gave up (must stay 0)
+  CTR_WOLF_OVERFLOW_RESET = 6,  // the part of CTR_WOLF_OVERFLOW dropped by a reset (initial wolves)
   kNumCounters = 8
 };
 
@@ -93,6 +94,8 @@ struct Params {
   int64_t env_base;
   int64_t B;
   int32_t eaten_cap;
+  int32_t wolf_cap;    // wolf rows per env (wab_config.wolf_slots); the wide kernel keeps the
+                       // first 8 in registers and the rest (rare) in their HBM rows
   // ---- state (device, SoA, env innermost)
   uint4* hdr;          // [B] {ostrich tile, turn, misc, episode (0xFFFFFFFF before the first reset)}
   double* food;        // [B]

@@ -566,7 +566,10 @@ __global__ __launch_bounds__(kThreads) void wab_kernel(Params p) {
           bits &= bits - 1;
           const uint32_t t = tiles[wd * 32 + b];
           if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = xy_pack(tile_dx(t), tile_dy(t));
-          else atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], 1ull);
+          else {
+            atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], 1ull);
+            atomicAdd(&p.counters[CTR_WOLF_OVERFLOW_RESET], 1ull);
+          }
         }
       }
       p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role, 0u, (uint32_t)n, 0u, 0u), ep);

@@ -446,7 +446,10 @@ __device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, cons
       const int b = __ffsll((unsigned long long)bits) - 1;
       bits &= bits - 1;
       if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = s.tiles[64 * half + b];
-      else wolf_of += 1;
+      else {
+        wolf_of += 1;
+        atomicAdd(&p.counters[CTR_WOLF_OVERFLOW_RESET], 1ull);
+      }
     }
   }
   p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);

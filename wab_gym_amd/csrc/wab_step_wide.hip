@@ -136,6 +136,40 @@ __device__ __forceinline__ uint32_t strip_bits(const Params& p, const WHead& h) 
   return bits;
 }
 
+// a wolf's tile after pursuit (:267-286): one axis step toward the ostrich, ties along x
+__device__ __forceinline__ uint32_t pursue(const Params& p, const WHead& h, uint32_t w) {
+  if (!p.wolves_can_move) return w;
+  int wx = xy_x(w), wy = xy_y(w);
+  const int ddx = h.ox - wx, ddy = h.oy - wy;
+  const bool alongx = abs(ddx) >= abs(ddy);
+  wx += alongx ? sgn(ddx) : 0;
+  wy += alongx ? 0 : sgn(ddy);
+  return xy_pack(wx, wy);
+}
+
+// The despawn draws (:262-264) of the wolves beyond the register slots, rows SLOTS..nw-1 (the
+// rare path: a ring spawn found every register slot taken).  Each is keyed like the register
+// ones: its tile, and its occurrence index among all wolves before it in row order, on their
+// pre-despawn positions (`wr` = rows 0..SLOTS-1, `live0` their mask).  Returns the survivors,
+// bit k - SLOTS.  Rows are re-read from HBM (one lane's loads, rarely more than a few).
+template <int SLOTS>
+__device__ __forceinline__ uint32_t spill_despawn(const Params& p, const WHead& h, int64_t g, int nw,
+                                               const uint32_t (&wr)[SLOTS], uint32_t live0) {
+  uint32_t keep = 0;
+  for (int k = SLOTS; k < nw && k < 32 + SLOTS; ++k) {
+    const uint32_t wk = p.wolves[(int64_t)k * p.B + g];
+    uint32_t occ = 0;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) occ += (((live0 >> t) & 1u) && wr[t] == wk) ? 1u : 0u;
+    for (int t = SLOTS; t < k; ++t) occ += p.wolves[(int64_t)t * p.B + g] == wk ? 1u : 0u;
+    const uint32_t ts = make_ts(SITE_DESPAWN, occ, h.turn);
+    const uint32_t h1 = fmix32(wk ^ h.b0);
+    const uint32_t hi = fmix32(h1 ^ ts ^ h.b1);
+    if (U_ge(h1, hi, ts, h.b0, p.keep_th, p.keep_tl)) keep |= 1u << (k - SLOTS);
+  }
+  return keep;
+}
+
 // dst[i] = src[i] for i < n by one wave, four independent loads per lane in flight at a time
 // (a plain strided loop waits for each load before its LDS store)
 template <typename T>
@@ -298,6 +332,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
   uint32_t live = 0;
+  uint32_t spill_live = 0;  // surviving wolves of rows SLOTS.. (bit k - SLOTS)
   int status = 0, ne = 0, ndep = 0;
   bool job = false, emptied = false;
   unsigned long long eaten_of = 0, wolf_of = 0;
@@ -373,6 +408,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
           }
           keep |= (kp & live4) << g4;
         }
+        // wolves beyond the SLOTS register slots (rows SLOTS..nw-1 of the same array, up to
+        // wolf_cap; a lane gets there only when a ring spawn found every register slot taken):
+        // their despawn draws, keyed like the others (occurrence among every wolf before it,
+        // pre-despawn positions)
+        if (nw > SLOTS) spill_live = spill_despawn<SLOTS>(p, h, g, nw, wr, live);
         live = keep;
       }
       // pursuit (:267-286): one axis step toward the ostrich, ties along x; the wolf grid of S
@@ -392,6 +432,15 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
         const int ddx = h.ox - wx, ddy = h.oy - wy;
         if (active && abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
         kill |= ddx == 0 && ddy == 0;
+      }
+      if (spill_live) {  // the surviving spilled wolves: pursuit, grid, kill (positions stay in HBM)
+        for (uint32_t bits = spill_live; bits; bits &= bits - 1u) {
+          const int k = SLOTS + __ffs(bits) - 1;
+          const uint32_t w = pursue(p, h, p.wolves[(int64_t)k * p.B + g]);
+          const int ddx = h.ox - xy_x(w), ddy = h.oy - xy_y(w);
+          if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
+          kill |= ddx == 0 && ddy == 0;
+        }
       }
       kill = kill && !p.god_mode;
       // the wolf grids of S are complete (this wave wrote every env's rows): plane 0 now,
@@ -480,6 +529,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
       WIDE_STAMP(5);
       // ------------------------------------------------ W0 P2: spawns, state of continuing envs
       if (active && !job) {
+        int n_unplaced = 0;
         if (p.wolves_on) {
           for (int w = 0; w < RW; ++w) {
             uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w];
@@ -491,7 +541,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
 #pragma unroll
               for (int k = 0; k < SLOTS; ++k)
                 if (!placed && !((live >> k) & 1u)) { wr[k] = t; live |= 1u << k; placed = true; }
-              if (!placed) wolf_of += 1;
+              n_unplaced += placed ? 0 : 1;  // every register slot taken: appended below
             }
           }
         }
@@ -499,6 +549,26 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
 #pragma unroll
         for (int k = 0; k < SLOTS; ++k)
           if ((live >> k) & 1u) p.wolves[(int64_t)(n++) * p.B + g] = wr[k];
+        if (spill_live | n_unplaced) {  // rare: compact the spilled survivors (row k is read
+                                        // before any row >= its new index is written), then
+                                        // the spawns that found no register slot
+          for (uint32_t bits = spill_live; bits; bits &= bits - 1u) {
+            const int k = SLOTS + __ffs(bits) - 1;
+            p.wolves[(int64_t)(n++) * p.B + g] = pursue(p, h, p.wolves[(int64_t)k * p.B + g]);
+          }
+          // the spawn tiles again, in the same order: the last n_unplaced of them
+          int skip = -n_unplaced;
+          for (int w = 0; w < RW; ++w)
+            for (uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w]; bits; bits &= bits - 1u) skip += 1;
+          for (int w = 0; w < RW && n_unplaced; ++w) {
+            for (uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w]; bits; bits &= bits - 1u) {
+              if (skip > 0) { skip -= 1; continue; }
+              const uint32_t t = xy_add(h.cpos, ring[32 * w + __ffs(bits) - 1]);
+              if (n < p.wolf_cap) p.wolves[(int64_t)(n++) * p.B + g] = t;
+              else wolf_of += 1;
+            }
+          }
+        }
         p.hdr[g] = make_uint4(h.cpos, (uint32_t)h.turn,
                               misc_pack((uint32_t)h.role, (uint32_t)status, (uint32_t)n, (uint32_t)ne, (uint32_t)ndep),
                               h.hdr.w);
@@ -713,8 +783,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
         while (bits) {
           const int j = __ffs(bits) - 1;
           bits &= bits - 1;
-          if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = xy_pack(p.cw - i, p.ch - j);
-          else wolf_of += 1;
+          if (n < p.wolf_cap) p.wolves[(int64_t)(n++) * p.B + g] = xy_pack(p.cw - i, p.ch - j);
+          else {
+            wolf_of += 1;
+            atomicAdd(&p.counters[CTR_WOLF_OVERFLOW_RESET], 1ull);
+          }
         }
       }
       p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
@@ -741,10 +814,6 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
 
 #define WAB_WIDE_INST(M, S) template __global__ void wab_step_wide<M, S>(Params);
 WAB_WIDE_INST(MODE_STEP, 8)
-WAB_WIDE_INST(MODE_STEP, 16)
-WAB_WIDE_INST(MODE_STEP, 32)
 WAB_WIDE_INST(MODE_RESET, 8)
-WAB_WIDE_INST(MODE_RESET, 16)
-WAB_WIDE_INST(MODE_RESET, 32)
 
 }  // namespace wab
