@@ -30,7 +30,7 @@ __global__ void wab_featurize_kernel(FeatParams p);
 __global__ void wab_featurize_small_kernel(FeatParams p);
 __global__ void wab_render_kernel(RenderParams p);
 __global__ void wab_egocentric_kernel(EgoParams p);
-template <int VEC>
+template <int VEC, int NE>
 __global__ void wab_returns_kernel(const float* __restrict__ reward, const uint8_t* __restrict__ done, int32_t T,
                                    int64_t B, double gamma, const float* __restrict__ bootstrap,
                                    float* __restrict__ out, RewardTable tab);
@@ -239,20 +239,51 @@ bool feat_small_ok(const Params& p) {
   return p.W * p.H <= 128 && p.S == p.H && max_dist < md;
 }
 
-// the discounted-return scan: four envs per thread when every [t] row is 16-byte aligned (B a
-// multiple of 4, aligned base pointers), else one
+// the discounted-return scan: VEC envs per thread, the widest whose grid still gives each of
+// the 1024 SIMDs a 64-thread wave and whose rows stay aligned; the reward table reduced to the
+// entries whose float32 is not the double itself (the others convert exactly)
 int launch_returns(const float* reward, const uint8_t* done, int32_t T, int64_t B, double gamma,
                    const float* bootstrap, float* returns, const wab::RewardTable& tab, void* stream) {
-  const bool vec4 = B % 4 == 0 && aligned16(reward) && aligned16(returns) && ((uintptr_t)done & 3u) == 0 &&
-                    ((uintptr_t)bootstrap & 3u) == 0;
-  const int64_t threads = vec4 ? B / 4 : B;
-  const dim3 grid((unsigned)((threads + 63) / 64));
-  if (vec4)
-    hipLaunchKernelGGL(wab::wab_returns_kernel<4>, grid, dim3(64), 0, (hipStream_t)stream, reward, done, T, B,
-                       gamma, bootstrap, returns, tab);
-  else
-    hipLaunchKernelGGL(wab::wab_returns_kernel<1>, grid, dim3(64), 0, (hipStream_t)stream, reward, done, T, B,
-                       gamma, bootstrap, returns, tab);
+  wab::RewardTable inexact;
+  std::memset(&inexact, 0, sizeof(inexact));
+  for (int k = 0; k < tab.n; ++k) {
+    float f;
+    std::memcpy(&f, &tab.f32[k], 4);
+    if ((double)f != tab.f64[k]) {
+      inexact.f32[inexact.n] = tab.f32[k];
+      inexact.f64[inexact.n] = tab.f64[k];
+      inexact.n++;
+    }
+  }
+  const auto fits = [&](int v) {
+    const uintptr_t a = 4u * (uintptr_t)v - 1u;
+    return B % v == 0 && B / v >= 64 * 1024 && ((uintptr_t)reward & a) == 0 && ((uintptr_t)returns & a) == 0 &&
+           ((uintptr_t)done & (uintptr_t)(v - 1)) == 0;
+  };
+  const int vec = fits(4) ? 4 : fits(2) ? 2 : 1;
+  const int ne = inexact.n <= 4 ? inexact.n : 8;
+  for (int k = inexact.n; k < ne; ++k) {  // pads: copies of entry 0 (same key, same value)
+    inexact.f32[k] = inexact.f32[0];
+    inexact.f64[k] = inexact.f64[0];
+  }
+  const dim3 grid((unsigned)((B / vec + 63) / 64));
+  hipStream_t s = (hipStream_t)stream;
+#define WAB_RET(V, N) \
+  hipLaunchKernelGGL((wab::wab_returns_kernel<V, N>), grid, dim3(64), 0, s, reward, done, T, B, gamma, bootstrap, returns, inexact)
+#define WAB_RET_NE(V) \
+  switch (ne) {                                                                                                   \
+    case 0: WAB_RET(V, 0); break;                                                                                 \
+    case 1: WAB_RET(V, 1); break;                                                                                 \
+    case 2: WAB_RET(V, 2); break;                                                                                 \
+    case 3: WAB_RET(V, 3); break;                                                                                 \
+    case 4: WAB_RET(V, 4); break;                                                                                 \
+    default: WAB_RET(V, 8);                                                                                       \
+  }
+  if (vec == 4) { WAB_RET_NE(4) }
+  else if (vec == 2) { WAB_RET_NE(2) }
+  else { WAB_RET_NE(1) }
+#undef WAB_RET_NE
+#undef WAB_RET
   HIP_TRY(hipGetLastError());
   return WAB_OK;
 }

@@ -297,19 +297,32 @@ __global__ __launch_bounds__(256) void wab_featurize_small_kernel(FeatParams p) 
 // actor_critic.finish_episode returns (actor_critic.py:139-143): R_t = r_t + gamma R_{t+1},
 // restarted after every done_t.  The scan is a serial chain in t, so each thread first issues
 // the loads of a whole chunk of kReturnsChunk steps (registers), then runs the chain; VEC
-// consecutive envs per thread (VEC = 4: one 16-byte reward and one 4-byte done load per step,
-// four independent chains).  64-thread workgroups: B = 65536 is 256 (VEC 4) or 1024 (VEC 1)
-// workgroups, so every CU holds a wave.  Double accumulation (the reference's Python floats),
-// no contraction (-ffp-contract=off), float32 out.
+// consecutive envs per thread (VEC independent chains, VEC-wide reward and done loads), VEC
+// chosen by the host so that the grid still gives every SIMD a wave (B = 65536: VEC 1, 1024
+// 64-thread workgroups).  Double accumulation (the reference's Python floats), no contraction
+// (-ffp-contract=off), float32 out.  `tab` holds only the rewards whose float32 is not their
+// double (wab_discounted_returns_exact; 0.1, 1.1 and -0.9 at the defaults): every other
+// float32 reward converts to its exact double as is.
 constexpr int kReturnsChunk = 32;
 
-template <int VEC>
+template <int VEC, int NE>
 __global__ __launch_bounds__(64) void wab_returns_kernel(const float* __restrict__ reward,
                                                          const uint8_t* __restrict__ done, int32_t T, int64_t B,
                                                          double gamma, const float* __restrict__ bootstrap,
                                                          float* __restrict__ out, RewardTable tab) {
   const int64_t b = ((int64_t)blockIdx.x * 64 + threadIdx.x) * VEC;
   if (b >= B) return;
+  // the NE table entries (the host pads to NE with copies of entry 0) in registers: a select
+  // on a scalar-register operand would first copy it to a vector register, per use
+  uint32_t tkey[NE > 0 ? NE : 1];
+  double tval[NE > 0 ? NE : 1];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    tkey[k] = tab.f32[k];
+    tval[k] = tab.f64[k];
+    opaque(tkey[k]);
+    opaque(tval[k]);
+  }
   double R[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) R[v] = bootstrap ? (double)bootstrap[b + v] : 0.0;
@@ -317,18 +330,22 @@ __global__ __launch_bounds__(64) void wab_returns_kernel(const float* __restrict
     const int n = hi + 1 < kReturnsChunk ? hi + 1 : kReturnsChunk;  // steps hi, hi-1, .., hi-n+1
     float rf[kReturnsChunk][VEC];
     uint32_t dn[kReturnsChunk];
+    // every load unconditional (a step past the segment's start re-reads step 0, unused): a
+    // load under `if (j < n)` becomes a branch with its own wait, one round trip per step
 #pragma unroll
     for (int j = 0; j < kReturnsChunk; ++j) {
-      if (j < n) {
-        const int64_t i = (int64_t)(hi - j) * B + b;
-        if constexpr (VEC == 4) {
-          const float4 r4 = *reinterpret_cast<const float4*>(reward + i);
-          rf[j][0] = r4.x; rf[j][1] = r4.y; rf[j][2] = r4.z; rf[j][3] = r4.w;
-          dn[j] = *reinterpret_cast<const uint32_t*>(done + i);
-        } else {
-          rf[j][0] = reward[i];
-          dn[j] = done[i];
-        }
+      const int64_t i = (int64_t)(hi - j > 0 ? hi - j : 0) * B + b;
+      if constexpr (VEC == 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(reward + i);
+        rf[j][0] = r4.x; rf[j][1] = r4.y; rf[j][2] = r4.z; rf[j][3] = r4.w;
+        dn[j] = *reinterpret_cast<const uint32_t*>(done + i);
+      } else if constexpr (VEC == 2) {
+        const float2 r2 = *reinterpret_cast<const float2*>(reward + i);
+        rf[j][0] = r2.x; rf[j][1] = r2.y;
+        dn[j] = *reinterpret_cast<const uint16_t*>(done + i);
+      } else {
+        rf[j][0] = reward[i];
+        dn[j] = done[i];
       }
     }
 #pragma unroll
@@ -342,14 +359,16 @@ __global__ __launch_bounds__(64) void wab_returns_kernel(const float* __restrict
           // else the float32 as given
           double r = (double)rf[j][v];
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (k < tab.n && __float_as_uint(rf[j][v]) == tab.f32[k]) r = tab.f64[k];
-          R[v] = r + gamma * R[v];
+          for (int k = 0; k < NE; ++k)
+            if (__float_as_uint(rf[j][v]) == tkey[k]) r = tval[k];
+          R[v] = r + gamma * R[v];  // (no contraction: -ffp-contract=off, the reference's op order)
           o[v] = (float)R[v];
         }
         const int64_t i = (int64_t)(hi - j) * B + b;
         if constexpr (VEC == 4)
           *reinterpret_cast<float4*>(out + i) = make_float4(o[0], o[1], o[2], o[3]);
+        else if constexpr (VEC == 2)
+          *reinterpret_cast<float2*>(out + i) = make_float2(o[0], o[1]);
         else
           out[i] = o[0];
       }
@@ -357,11 +376,41 @@ __global__ __launch_bounds__(64) void wab_returns_kernel(const float* __restrict
   }
 }
 
-template __global__ void wab_returns_kernel<1>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
-                                               int64_t, double, const float* __restrict__, float* __restrict__,
-                                               RewardTable);
-template __global__ void wab_returns_kernel<4>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
-                                               int64_t, double, const float* __restrict__, float* __restrict__,
-                                               RewardTable);
+template __global__ void wab_returns_kernel<1, 0>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<1, 1>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<1, 2>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<1, 3>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<1, 4>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<1, 8>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<2, 0>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<2, 1>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<2, 2>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<2, 3>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<2, 4>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<2, 8>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<4, 0>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<4, 1>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<4, 2>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<4, 3>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<4, 4>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
+template __global__ void wab_returns_kernel<4, 8>(const float* __restrict__, const uint8_t* __restrict__, int32_t,
+    int64_t, double, const float* __restrict__, float* __restrict__, RewardTable);
 
 }  // namespace wab
