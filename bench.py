@@ -200,6 +200,9 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="graph", choices=["graph", "launch"])
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="T > 0: wab_rollout segments of T steps (one launch each; obs, reward, done "
+                         "into a [T, B] rollout buffer) instead of one wab_step launch per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
@@ -250,6 +253,9 @@ def main():
         desc = desc % C5_SEGMENT
         K = max(C5_SEGMENT, K // C5_SEGMENT * C5_SEGMENT)  # whole segments
         W = max(C5_SEGMENT, -(-W // C5_SEGMENT) * C5_SEGMENT)
+    elif args.rollout > 0:
+        K = max(args.rollout, K // args.rollout * args.rollout)  # whole segments
+        W = -(-W // args.rollout) * args.rollout
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
@@ -289,6 +295,21 @@ def main():
                 if i == T - 1:
                     _lib.check(L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s),
                                "wab_discounted_returns_exact")
+    elif args.rollout > 0:
+        T = args.rollout
+        seq_planes = torch.empty((T, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+        seq_scal = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
+        seq_rew = torch.empty((T, B), dtype=torch.float32, device=dev)
+        seq_done = torch.empty((T, B), dtype=torch.uint8, device=dev)
+        seq = _lib.WabObs(seq_planes.data_ptr(), seq_scal[0].data_ptr(), seq_scal[1].data_ptr(),
+                          seq_scal[2].data_ptr())
+        seq_addr = ctypes.addressof(seq)
+
+        def run(t0, n, stream):
+            s = ctypes.c_void_p(stream.cuda_stream)
+            for t in range(t0, t0 + n, T):
+                _lib.check(L.wab_rollout(h, a0 + t * B, T, seq_addr, seq_rew.data_ptr(), seq_done.data_ptr(), s),
+                           "wab_rollout")
     else:
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)

@@ -2,7 +2,7 @@
 
 Compiles wab_step_small.hip with -DWAB_ONLY_WAVE=k (the other waves' functions dead-code
 eliminated; not a runnable build) and counts VALU / SALU / LDS / VMEM instructions of the
-default-geometry kernel wab_step_small<8, 11, false>, plus the store-only remainder (k = 9).
+default-geometry kernel wab_step_small<8, 11, false, false>, plus the store-only remainder (k = 9).
 Loops count once, so this ranks the straight-line cost of each wave's step, the part a
 PMC run cannot split by wave.  Usage: python tools/isa_count.py [extra hipcc flags]
 """
@@ -13,7 +13,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "wab_gym_amd", "csrc", "wab_step_small.hip")
-KERNEL = "_ZN3wab14wab_step_smallILi8ELi11ELb0EEEvNS_6ParamsE"
+KERNEL = "_ZN3wab14wab_step_smallILi8ELi11ELb0ELb0EEEvNS_6ParamsE"
 
 
 def counts(flags):

@@ -21,7 +21,7 @@
 namespace wab {
 template <int MODE, int SLOTS, bool SMALL>
 __global__ void wab_kernel(Params p);
-template <int SLOTS, int G, bool FEAT>
+template <int SLOTS, int G, bool FEAT, bool ROLL>
 __global__ void wab_step_small(Params p);
 template <int MODE, int SLOTS>
 __global__ void wab_step_wide(Params p);
@@ -158,23 +158,24 @@ void* wide_kernel_ptr(int) {
   return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, kWideRegSlots>);
 }
 
-template <int G>
+template <int G, bool ROLL = false>
 void* small_kernel_ptr(int slots) {
   switch (slots) {
-    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8, G, false>);
-    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16, G, false>);
-    default: return reinterpret_cast<void*>(&wab::wab_step_small<32, G, false>);
+    case 8: return reinterpret_cast<void*>(&wab::wab_step_small<8, G, false, ROLL>);
+    case 16: return reinterpret_cast<void*>(&wab::wab_step_small<16, G, false, ROLL>);
+    default: return reinterpret_cast<void*>(&wab::wab_step_small<32, G, false, ROLL>);
   }
 }
 
-template <int G, bool FEAT = false>
+// ROLL: the multi-step build (Params::n_steps steps per launch, wab_rollout)
+template <int G, bool FEAT = false, bool ROLL = false>
 void launch_small(wab_handle* h, const Params& p, hipStream_t stream) {
   const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
   const size_t lds = FEAT ? h->small_feat_lds_bytes : h->small_lds_bytes;
   switch (h->slots) {
-    case 8: hipLaunchKernelGGL((wab::wab_step_small<8, G, FEAT>), grid, block, lds, stream, p); break;
-    case 16: hipLaunchKernelGGL((wab::wab_step_small<16, G, FEAT>), grid, block, lds, stream, p); break;
-    default: hipLaunchKernelGGL((wab::wab_step_small<32, G, FEAT>), grid, block, lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((wab::wab_step_small<8, G, FEAT, ROLL>), grid, block, lds, stream, p); break;
+    case 16: hipLaunchKernelGGL((wab::wab_step_small<16, G, FEAT, ROLL>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((wab::wab_step_small<32, G, FEAT, ROLL>), grid, block, lds, stream, p); break;
   }
 }
 
@@ -186,8 +187,14 @@ int launch(wab_handle* h, const Params& p, hipStream_t stream) {
     const size_t lds = h->wide_lds_bytes;
     hipLaunchKernelGGL((wab::wab_step_wide<MODE, kWideRegSlots>), grid, block, lds, stream, p);
   } else if (MODE == 0 && h->step_kernel == KERNEL_SMALL) {
-    if (h->small_g11) launch_small<11>(h, p, stream);
-    else launch_small<0>(h, p, stream);
+    if (p.n_steps > 1) {
+      if (h->small_g11) launch_small<11, false, true>(h, p, stream);
+      else launch_small<0, false, true>(h, p, stream);
+    } else if (h->small_g11) {
+      launch_small<11>(h, p, stream);
+    } else {
+      launch_small<0>(h, p, stream);
+    }
   } else if (small_map(p)) launch_as<MODE, true>(h, p, stream);
   else launch_as<MODE, false>(h, p, stream);
   HIP_TRY(hipGetLastError());
@@ -489,6 +496,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   h->device = device;
   h->slots = slots;
   p.wolf_cap = slots;
+  p.n_steps = 1;
   h->n_blocks = (int)((batch + wab::kEnvsPerBlock - 1) / wab::kEnvsPerBlock);
   h->lds_bytes = (size_t)wab::lds_layout(p, slots).total * 4u;
   {
@@ -604,8 +612,10 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_lds_bytes);
   }
   if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
-    e = hipFuncSetAttribute(h->small_g11 ? small_kernel_ptr<11>(slots) : small_kernel_ptr<0>(slots),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->small_lds_bytes);
+    for (void* k : {h->small_g11 ? small_kernel_ptr<11>(slots) : small_kernel_ptr<0>(slots),
+                    h->small_g11 ? small_kernel_ptr<11, true>(slots) : small_kernel_ptr<0, true>(slots)})
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->small_lds_bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     std::string msg = std::string("wab_create: ") + hipGetErrorString(e);
@@ -679,6 +689,21 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
   if (int rc = check_obs(obs_seq, "wab_rollout")) return rc;
   const int64_t B = h->p.B;
   const size_t OB = (size_t)h->p.OB;
+  if (T > 0 && h->step_kernel == KERNEL_SMALL && h->reset_done && actions && reward && done &&
+      ((size_t)B * OB) % 16u == 0) {  // (every step's planes 16-byte aligned)
+    // one launch: each workgroup runs its 64 envs through the T steps (Params::n_steps)
+    Params p = h->p;
+    p.actions = actions;
+    p.planes = obs_seq->planes;
+    p.food_turns = obs_seq->food_turns;
+    p.role = obs_seq->role;
+    p.status = obs_seq->status;
+    p.reward = reward;
+    p.done = done;
+    p.n_steps = T;
+    DeviceGuard guard(h->device);
+    return launch<0>(h, p, (hipStream_t)stream);
+  }
   for (int32_t t = 0; t < T; ++t) {
     wab_obs o;
     o.planes = obs_seq->planes + (size_t)t * (size_t)B * OB;

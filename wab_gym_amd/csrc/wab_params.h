@@ -94,6 +94,8 @@ struct Params {
   int64_t env_base;
   int64_t B;
   int32_t eaten_cap;
+  int32_t n_steps;     // steps per launch (wab_rollout on the small kernel: the I/O arrays are
+                       // [n_steps][...], step t at offset t * B; 1 otherwise)
   int32_t wolf_cap;    // wolf rows per env (wab_config.wolf_slots); the wide kernel keeps the
                        // first 8 in registers and the rest (rare) in their HBM rows
   // ---- state (device, SoA, env innermost)

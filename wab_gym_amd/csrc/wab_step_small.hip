@@ -1099,8 +1099,21 @@ __device__ __forceinline__ Params wave_params(const Params& p0) {
   return p;
 }
 
-template <int SLOTS, int G, bool FEAT>
-__global__ __launch_bounds__(256) void wab_step_small(Params p0) {
+// step t of a multi-step launch (Params::n_steps): the I/O arrays advanced to their [t] slices
+__device__ __forceinline__ void step_slice(Params& p, int t) {
+  if (t == 0) return;
+  const int64_t o = (int64_t)t * p.B;
+  p.actions += o;
+  if (p.planes) p.planes += o * p.OB;
+  p.food_turns += o;
+  p.role += o;
+  p.status += o;
+  p.reward += o;
+  p.done += o;
+}
+
+template <int SLOTS, int G, bool FEAT, bool ROLL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 1))) void wab_step_small(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 #ifdef WAB_STAMPS
   uint64_t t_entry;  // before the first kernel-argument load
@@ -1117,48 +1130,81 @@ __global__ __launch_bounds__(256) void wab_step_small(Params p0) {
   }
 #endif
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (uniform branches)
-  unsigned long long jm;  // the group's done envs (every wave computes the same mask)
 #ifdef WAB_ONLY_WAVE  // static per-wave instruction counts (tools/isa_count.py); not a runnable build
   if (wave != WAB_ONLY_WAVE) return;
 #endif
-  if (wave == 0) {
-    // the bushes wave carries the longest chain and shares its SIMD with three helper waves
-    // of other groups: let the arbiter issue its instructions first
-    __builtin_amdgcn_s_setprio(3);
+  if constexpr (!ROLL) {
+    unsigned long long jm;  // the group's done envs (every wave computes the same mask)
+    if (wave == 0) {
+      // the bushes wave carries the longest chain and shares its SIMD with three helper waves
+      // of other groups: let the arbiter issue its instructions first
+      __builtin_amdgcn_s_setprio(3);
+      const Params p = wave_params<G, FEAT>(p0);
+      jm = bushes_wave<SLOTS, G>(p, small_layout(p), lds, lane);
+      __builtin_amdgcn_s_setprio(0);
+    } else if (wave == 1) {
+      const Params p = wave_params<G, FEAT>(p0);
+      jm = draws_wave<G>(p, small_layout(p), lds, lane);
+    } else if (wave == 2) {
+      const Params p = wave_params<G, FEAT>(p0);
+      jm = wolves_wave<SLOTS, G>(p, small_layout(p), lds, lane);
+    } else {
+      const Params p = wave_params<G, FEAT>(p0);
+      jm = ring_wave<SLOTS, G>(p, small_layout(p), lds, lane);
+    }
     const Params p = wave_params<G, FEAT>(p0);
-    jm = bushes_wave<SLOTS, G>(p, small_layout(p), lds, lane);
-    __builtin_amdgcn_s_setprio(0);
-  } else if (wave == 1) {
-    const Params p = wave_params<G, FEAT>(p0);
-    jm = draws_wave<G>(p, small_layout(p), lds, lane);
-  } else if (wave == 2) {
-    const Params p = wave_params<G, FEAT>(p0);
-    jm = wolves_wave<SLOTS, G>(p, small_layout(p), lds, lane);
+    const SmallLayout L = small_layout(p);
+    if (!FEAT && early_obs(p)) {  // the units that touch a done env (the rest went out after B1)
+      if (jm) store_units(p, lds + L.stream, jm, true, wave, 4, lane);
+    } else if (!FEAT || p.planes) {
+      store_obs(p, lds + L.stream, threadIdx.x);
+    }
+    if constexpr (FEAT) step_features(p, L, lds, wave, lane);
   } else {
-    const Params p = wave_params<G, FEAT>(p0);
-    jm = ring_wave<SLOTS, G>(p, small_layout(p), lds, lane);
+    // wab_rollout: n_steps steps of this group, one after the other (the envs of a workgroup
+    // depend on nothing outside it); the state goes through HBM as between launches, every
+    // store of step t complete (vmcnt) before step t + 1 reads it
+    for (int t = 0; t < p0.n_steps; ++t) {
+      if (t > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      Params p = wave_params<G, false>(p0);
+      step_slice(p, t);
+      const SmallLayout L = small_layout(p);
+      if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        bushes_wave<SLOTS, G>(p, L, lds, lane);
+        __builtin_amdgcn_s_setprio(0);
+      } else if (wave == 1) {
+        draws_wave<G>(p, L, lds, lane);
+      } else if (wave == 2) {
+        wolves_wave<SLOTS, G>(p, L, lds, lane);
+      } else {
+        ring_wave<SLOTS, G>(p, L, lds, lane);
+      }
+      store_obs(p, lds + L.stream, threadIdx.x);
+    }
   }
-  const Params p = wave_params<G, FEAT>(p0);
-  const SmallLayout L = small_layout(p);
-  if (!FEAT && early_obs(p)) {  // the units that touch a done env (the rest went out after B1)
-    if (jm) store_units(p, lds + L.stream, jm, true, wave, 4, lane);
-  } else if (!FEAT || p.planes) {
-    store_obs(p, lds + L.stream, threadIdx.x);
-  }
-  if constexpr (FEAT) step_features(p, L, lds, wave, lane);
 }
 
-template __global__ void wab_step_small<8, 0, false>(Params);
-template __global__ void wab_step_small<16, 0, false>(Params);
-template __global__ void wab_step_small<32, 0, false>(Params);
-template __global__ void wab_step_small<8, 11, false>(Params);
-template __global__ void wab_step_small<16, 11, false>(Params);
-template __global__ void wab_step_small<32, 11, false>(Params);
-template __global__ void wab_step_small<8, 0, true>(Params);
-template __global__ void wab_step_small<16, 0, true>(Params);
-template __global__ void wab_step_small<32, 0, true>(Params);
-template __global__ void wab_step_small<8, 11, true>(Params);
-template __global__ void wab_step_small<16, 11, true>(Params);
-template __global__ void wab_step_small<32, 11, true>(Params);
+template __global__ void wab_step_small<8, 0, false, false>(Params);
+template __global__ void wab_step_small<8, 0, true, false>(Params);
+template __global__ void wab_step_small<8, 0, false, true>(Params);
+template __global__ void wab_step_small<8, 11, false, false>(Params);
+template __global__ void wab_step_small<8, 11, true, false>(Params);
+template __global__ void wab_step_small<8, 11, false, true>(Params);
+template __global__ void wab_step_small<16, 0, false, false>(Params);
+template __global__ void wab_step_small<16, 0, true, false>(Params);
+template __global__ void wab_step_small<16, 0, false, true>(Params);
+template __global__ void wab_step_small<16, 11, false, false>(Params);
+template __global__ void wab_step_small<16, 11, true, false>(Params);
+template __global__ void wab_step_small<16, 11, false, true>(Params);
+template __global__ void wab_step_small<32, 0, false, false>(Params);
+template __global__ void wab_step_small<32, 0, true, false>(Params);
+template __global__ void wab_step_small<32, 0, false, true>(Params);
+template __global__ void wab_step_small<32, 11, false, false>(Params);
+template __global__ void wab_step_small<32, 11, true, false>(Params);
+template __global__ void wab_step_small<32, 11, false, true>(Params);
 
 }  // namespace wab
