@@ -156,6 +156,7 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) 
 // workgroup (dwords)
 struct SmallLayout {
   uint32_t tiles, thr, gap, stream, stream_words, cval, flag, wolfp, kill, bushp, strip, gone, info, spawn, jbm, jkey;
+  uint32_t carry, act;  // multi-step launches: the new episodes' state for the next step, its actions
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
 };
 
@@ -178,6 +179,8 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.spawn = o; o += 64u * 4u;
   L.jbm = o; o += 64u * 4u;
   L.jkey = o; o += 2u * 2u * 64u;
+  L.carry = o; o += 8u * 64u;  // per env: role | new wolves << 8, food (2), wolf cells (4), pad
+  L.act = o; o += 16u;         // 64 int8 actions
   L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.fbits = L.ftab = L.fzero = L.scal = o;

@@ -273,6 +273,8 @@ struct Lds {
   uint32_t* jbm;    // [job][4] reset bush bitmaps (W1, W3)
   uint32_t* jkey;   // [2][job][2] the new episodes' keys: W1's copy, W3's copy
   uint32_t* scal;   // [64] fused features: food_turns | role << 8 | status << 16 of the obs
+  uint32_t* carry;  // [64][8] multi-step launches: a new episode's role | wolves << 8, food, wolf cells (W3)
+  uint32_t* act;    // [16] multi-step launches: the next step's 64 actions (W1)
 };
 
 __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
@@ -293,6 +295,8 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   s.jbm = lds + L.jbm;
   s.jkey = lds + L.jkey;
   s.scal = lds + L.scal;
+  s.carry = lds + L.carry;
+  s.act = lds + L.act;
   return s;
 }
 
@@ -309,6 +313,15 @@ __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u
 #ifndef WAB_P1_PRIO
 #define WAB_P1_PRIO 1
 #endif
+// issue priorities in multi-step launches (A/B): 0 none, 1 as a single step with W3 back at 0
+// when a step starts, 2 as a single step
+#ifndef WAB_ROLL_PRIO
+#define WAB_ROLL_PRIO 1
+#endif
+#define WAB_PRIO(ROLL, V)                                             \
+  do {                                                                \
+    if (!(ROLL) || WAB_ROLL_PRIO != 0) __builtin_amdgcn_s_setprio(V); \
+  } while (0)
 
 // the entering strip's cells are drawn in two parts, [0, kStripW1) on W1 after the tile value
 // and the rest on W3 after the spawn set (A/B: -DWAB_STRIP_W1=k)
@@ -414,16 +427,85 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
   }
 }
 
-// The new episode of a done env (reset :231-248, spawn_ostriches :595-611): state, scalars,
-// initial wolves (initialize_wolves :578-593: the view's spawn set at turn 0), and its obs
-// segment (which must be clear) from the job's reset draws.
+// --------------------------------------------------------------------------- multi-step launches
+// wab_rollout runs its T steps in one launch (ROLL): each wave keeps its part of an env's state
+// in registers from one step to the next (its view of the header; W0 also the food, the view
+// bitmap and the first four eaten-log entries; W2 the wolf slots, uncompacted, with a live
+// mask), a done env's new episode comes from W3 through LDS (Lds::carry), the next step's
+// actions from W1 through LDS (Lds::act, one scalar load per group).  Only the first step
+// loads state from HBM and only the last stores it; in between, a step issues no vector load
+// on its common path, so nothing waits for the previous step's obs stores to drain.
+struct CarryHdr {
+  uint4 hdr;  // the env's header at the start of the next step, as far as this wave uses it
+};
+struct CarryW0 {
+  uint4 hdr;
+  double food;
+  uint32_t bw[4];            // view bitmap (post-eat)
+  uint32_t lxy[4], lrem[4];  // eaten-log entries 0..3 (entries >= 4 stay in HBM)
+};
+template <int SLOTS>
+struct CarryW2 {
+  uint4 hdr;
+  uint32_t wr[SLOTS];  // wolf tiles, uncompacted
+  uint32_t live;       // occupied slots
+};
+
+__device__ __forceinline__ int act_of(const Lds& s, int lane) {
+  return (int)reinterpret_cast<const int8_t*>(s.act)[lane];
+}
+
+// the next step's actions of the group into Lds::act: one 64-byte scalar load (scalar loads
+// count in lgkmcnt, so no wait on this wave's stores), spread over lanes 0..15; a partial or
+// misaligned group reads per lane
+__device__ __forceinline__ void prefetch_actions(const Params& p, const Lds& s, int lane) {
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const int8_t* a = p.actions + p.B + g0;  // step t + 1 (p.actions is step t's slice)
+  if (g0 + 64 <= p.B && (reinterpret_cast<uintptr_t>(a) & 3u) == 0u) {
+    typedef const uint32_t __attribute__((address_space(4))) CU32;
+    CU32* c = (CU32*)reinterpret_cast<uintptr_t>(a);
+    asm volatile("" : "+s"(c));
+    uint32_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = c[k];
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d = lane == k ? v[k] : d;
+    if (lane < 16) s.act[lane] = d;
+  } else {
+    const int8_t v = g0 + lane < p.B ? a[lane] : (int8_t)0;
+    reinterpret_cast<int8_t*>(s.act)[lane] = v;
+  }
+}
+
+// a done env's new episode as W3 left it in Lds::carry (after B2)
+struct NewEp {
+  uint32_t role, nw;
+  double food;
+  M128 wolves;  // wolf cells of the view
+};
+__device__ __forceinline__ NewEp carry_of(const Lds& s, int lane) {
+  const uint4 a = *reinterpret_cast<const uint4*>(&s.carry[8 * lane]);
+  const uint4 b = *reinterpret_cast<const uint4*>(&s.carry[8 * lane + 4]);
+  NewEp n;
+  n.role = a.x & 0xFFu;
+  n.nw = (a.x >> 8) & 0xFFu;
+  n.food = __longlong_as_double((long long)((uint64_t)a.y | ((uint64_t)a.z << 32)));
+  n.wolves = m_make(a.w, b.x, b.y, b.z);
+  return n;
+}
+__device__ __forceinline__ uint4 new_header(const NewEp& n, const Head& h) {
+  return make_uint4(xy_pack(0, 0), 0u, misc_pack(n.role, 0u, n.nw, 0u, 0u), h.hdr.w + 1u);
+}
+
 // The new episode of a done env (reset :231-248, spawn_ostriches :595-611) in two parts: A
 // needs only the new key (state, scalars, initial wolves = the view's spawn set at turn 0,
 // initialize_wolves :578-593, and the wolf and ostrich planes of its obs segment, which must
 // be clear); B the job's reset bush draws (bushmap, bush plane).  Returns the new role.
-template <int SLOTS>
+template <int SLOTS, bool ROLL = false>
 __device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, const Head& h, int64_t g, uint32_t kb0,
-                                             uint32_t kb1, uint32_t ebit, unsigned long long& wolf_of) {
+                                             uint32_t kb1, uint32_t ebit, unsigned long long& wolf_of,
+                                             bool last = true) {
   const double food2 = p.start_food_random
                            ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
                            : p.start_food;
@@ -438,6 +520,7 @@ __device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, cons
     stream_or128(s.stream, ebit, wp);
   }
   stream_set_ostrich(p, s.stream, ebit, role2);
+  const bool store = !ROLL || last;  // (ROLL: the state stays on chip until the last step)
   int n = 0;  // initial wolves, one per wolf cell of the view (slot order is irrelevant)
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -445,15 +528,26 @@ __device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, cons
     while (bits) {
       const int b = __ffsll((unsigned long long)bits) - 1;
       bits &= bits - 1;
-      if (n < SLOTS) p.wolves[(int64_t)(n++) * p.B + g] = s.tiles[64 * half + b];
-      else {
+      if (n < SLOTS) {
+        if (store) p.wolves[(int64_t)n * p.B + g] = s.tiles[64 * half + b];
+        n += 1;
+      } else {
         wolf_of += 1;
         atomicAdd(&p.counters[CTR_WOLF_OVERFLOW_RESET], 1ull);
       }
     }
   }
-  p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
-  p.food[g] = food2;
+  if (store) {
+    p.hdr[g] = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
+    p.food[g] = food2;
+  }
+  if constexpr (ROLL) {  // for the next step's waves (the wolves as cells: W2 takes the first SLOTS)
+    const uint64_t fb = (uint64_t)__double_as_longlong(food2);
+    uint32_t* c = &s.carry[8 * (int)(g & 63)];
+    *reinterpret_cast<uint4*>(c) = make_uint4((uint32_t)role2 | ((uint32_t)n << 8), (uint32_t)fb, (uint32_t)(fb >> 32),
+                                              m_word<0>(nwm));
+    *reinterpret_cast<uint4*>(c + 4) = make_uint4(m_word<1>(nwm), m_word<2>(nwm), m_word<3>(nwm), 0u);
+  }
   const uint32_t ft2 = (uint32_t)(int)ceil(food2 * (double)p.turns_empty);
   p.food_turns[g] = (uint8_t)ft2;
   p.role[g] = (uint8_t)role2;
@@ -463,9 +557,10 @@ __device__ __forceinline__ int new_episode_a(const Params& p, const Lds& s, cons
 }
 
 __device__ __forceinline__ void new_episode_b(const Params& p, const Lds& s, int64_t g, int j, uint32_t ebit,
-                                              int role2) {
+                                              int role2, bool store = true) {
   const M128 nbm = m_unpack(*reinterpret_cast<const uint4*>(&s.jbm[4 * j]));
   stream_or128(s.stream, ebit + (uint32_t)p.WH, p.restrict_view ? m_andn(nbm, view_mask_of(p, role2)) : nbm);
+  if (!store) return;  // (ROLL: W0 takes the bitmap from jbm itself)
   p.bushmap[g] = m_word<0>(nbm);
   if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(nbm);
   if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(nbm);
@@ -483,8 +578,9 @@ __device__ __forceinline__ void early_view_zeros(const Params& p, uint32_t e0, u
 }
 
 // --------------------------------------------------------------------------- W0: bushes
-template <int SLOTS, int G>
-__device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+template <int SLOTS, int G, bool ROLL = false>
+__device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane,
+                                                          CarryW0* carry = nullptr, int t = 0, bool last = true) {
   const Lds s = lds_of(lds, L);
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const int64_t g = g0 + lane;
@@ -497,7 +593,22 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   double food = 0.0;
   uint32_t bw0 = 0u, bw1 = 0u, bw2 = 0u, bw3 = 0u;
   uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
-  HeadRaw hr = head_fetch(p, g, active);
+  HeadRaw hr;
+  if (ROLL && t > 0) {  // (multi-step launch: the state this wave carried from the last step)
+    hr.hdr = carry->hdr;
+    hr.a = act_of(s, lane);
+    food = carry->food;
+    bw0 = carry->bw[0];
+    bw1 = carry->bw[1];
+    bw2 = carry->bw[2];
+    bw3 = carry->bw[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lxy[i] = carry->lxy[i];
+      lrem[i] = carry->lrem[i];
+    }
+  } else {
+  hr = head_fetch(p, g, active);
   {  // (unconditional: an inactive lane reads env 0; entries at or past eaten_cap read the
      // last entry and are never used, entry i counts only below the log length <= cap)
     const int64_t gl = active ? g : 0;
@@ -524,21 +635,25 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     opaque(lxy[i]);
     opaque(lrem[i]);
   }
+  }
   if (!active) {  // (env 0's values: an inactive lane must not eat, log or store anything)
     food = 0.0;
     bw0 = bw1 = bw2 = bw3 = 0u;
   }
-  {
+  // (multi-step launches after step 0: the stream was cleared by the threads that stored it,
+  // the flags by W1 after B2, the LDS tables are still there: no B_init)
+  const bool init = !ROLL || t == 0;
+  if (init) {
     uint4* z = reinterpret_cast<uint4*>(s.stream);
     for (uint32_t i = lane; i < L.stream_words / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const Head h = head_decode(p, g, active, hr);
-  if (lane == 0) {
+  if (lane == 0 && init) {
     s.flag[0] = 0u;
     s.flag[1] = 0u;
     s.flag[2] = 0u;
   }
-  lds_barrier();  // B_init: the hand-off flags are clear
+  if (init) lds_barrier();  // B_init: the hand-off flags are clear
   int ne = (int)misc_ne(h.hdr.z), ndep = (int)misc_ndep(h.hdr.z);
   const int status_old = (int)misc_status(h.hdr.z);
   const int role = h.role;
@@ -570,13 +685,14 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   bool center_bush = m_test(bm, ccb);
   if (ne > 4 && (center_bush || (ndep > 0 && h.dir != DIR_STAY))) {
     for (int i0 = 4; i0 < ne; i0 += 4) {
+      uint32_t exy[4] = {0u, 0u, 0u, 0u}, erem[4] = {0u, 0u, 0u, 0u};  // (entries 0..3 stay in lxy, lrem)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (i0 + k < ne) {
-          lxy[k] = p.eaten_xy[(int64_t)(i0 + k) * p.B + g];
-          lrem[k] = p.eaten_rem[(int64_t)(i0 + k) * p.B + g];
+          exy[k] = p.eaten_xy[(int64_t)(i0 + k) * p.B + g];
+          erem[k] = p.eaten_rem[(int64_t)(i0 + k) * p.B + g];
         }
-      scan_log(p, h, lxy, lrem, i0, ne, found, found_rem, gone);
+      scan_log(p, h, exy, erem, i0, ne, found, found_rem, gone);
     }
     bm = m_andn(bm, gone);
     center_bush = m_test(bm, ccb);
@@ -600,7 +716,19 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     food = food < 0.0 ? 0.0 : (food > 1.0 ? 1.0 : food);
     reward += p.r_eat;
     bool logged = true;
-    if (found >= 0) {
+    if (ROLL && found >= 0 && found < 4) {  // (entries 0..3 live in registers)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (found == k) lrem[k] = (uint32_t)(rem - 1);
+    } else if (ROLL && found < 0 && ne < 4 && ne < p.eaten_cap) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (ne == k) {
+          lxy[k] = h.cpos;
+          lrem[k] = (uint32_t)(rem - 1);
+        }
+      ne += 1;
+    } else if (found >= 0) {
       p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
     } else if (ne < p.eaten_cap) {
       p.eaten_xy[(int64_t)ne * p.B + g] = h.cpos;
@@ -621,7 +749,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
   SMALL_STAMP(3);
   lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
-  if constexpr (WAB_P1_PRIO) __builtin_amdgcn_s_setprio(1);
+  if constexpr (WAB_P1_PRIO) WAB_PRIO(ROLL, 1);
 
   // status (starve overrides kill), reward/done (:328-340), scalars, bushes and food
   const bool killed = s.kill[lane] != 0u;
@@ -650,11 +778,13 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     if (p.features && !job) s.scal[lane] = (uint32_t)ft | ((uint32_t)role << 8) | ((uint32_t)status << 16);
     if (!job) {
       bm = m_or(bm, m_andn(strip_of(p, s, lane, h.dir), gone));
-      p.bushmap[g] = m_word<0>(bm);
-      if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(bm);
-      if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(bm);
-      if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(bm);
-      p.food[g] = food;
+      if (!ROLL || last) {
+        p.bushmap[g] = m_word<0>(bm);
+        if (p.WHW > 1) p.bushmap[p.B + g] = m_word<1>(bm);
+        if (p.WHW > 2) p.bushmap[2 * p.B + g] = m_word<2>(bm);
+        if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(bm);
+        p.food[g] = food;
+      }
     }
   }
   if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
@@ -693,18 +823,59 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     lds_barrier();  // B3
   }
+  if constexpr (ROLL) {
+    if (!last) {  // this wave's state for the next step (a new episode's from W3 and jbm)
+      if (job) {
+        const NewEp n = carry_of(s, lane);
+        const int j = __popcll(jm & ((1ull << lane) - 1ull));
+        const uint4 nb = *reinterpret_cast<const uint4*>(&s.jbm[4 * j]);
+        carry->hdr = new_header(n, h);
+        carry->food = n.food;
+        carry->bw[0] = nb.x;
+        carry->bw[1] = nb.y;
+        carry->bw[2] = nb.z;
+        carry->bw[3] = nb.w;
+      } else {
+        carry->hdr = make_uint4(h.cpos, (uint32_t)h.turn, misc_pack((uint32_t)role, (uint32_t)status, 0u, (uint32_t)ne,
+                                                                    (uint32_t)ndep), h.hdr.w);
+        carry->food = food;
+        carry->bw[0] = m_word<0>(bm);
+        carry->bw[1] = m_word<1>(bm);
+        carry->bw[2] = m_word<2>(bm);
+        carry->bw[3] = m_word<3>(bm);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        carry->lxy[i] = lxy[i];
+        carry->lrem[i] = lrem[i];
+      }
+    } else if (active && !job) {  // the eaten-log entries kept in registers
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < ne && i < p.eaten_cap) {
+          p.eaten_xy[(int64_t)i * p.B + g] = lxy[i];
+          p.eaten_rem[(int64_t)i * p.B + g] = (uint8_t)lrem[i];
+        }
+    }
+  }
   SMALL_STAMP(5);
   return jm;
 }
 
 // --------------------------------------------------------------------------- W1: draws
-template <int G>
-__device__ __forceinline__ unsigned long long draws_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+template <int G, bool ROLL = false>
+__device__ __forceinline__ unsigned long long draws_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane,
+                                                         CarryHdr* carry = nullptr, int t = 0, bool last = true) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(10);
-  __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
-  HeadRaw hr = head_fetch(p, g, g < p.B);
+  WAB_PRIO(ROLL, 2);  // the tile value is on the bushes wave's path
+  HeadRaw hr;
+  if (ROLL && t > 0) {  // (multi-step launch: the thresholds are in LDS since step 0)
+    hr.hdr = carry->hdr;
+    hr.a = act_of(s, lane);
+  } else {
+  hr = head_fetch(p, g, g < p.B);
   {  // every threshold load in flight at once (a copy loop waits for each before the next)
     const int nthr = p.max_berries;  // <= 255
     uint64_t tv[4];
@@ -718,8 +889,9 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
       if (64 * k + lane < nthr) s.thr[64 * k + lane] = tv[k];
     if (lane == 0) bush_thr_pads(s.thr, nthr);
   }
+  }
   const Head h = head_decode(p, g, g < p.B, hr);
-  lds_barrier();  // B_init
+  if (!ROLL || t == 0) lds_barrier();  // B_init
   SMALL_STAMP(30);
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
@@ -728,7 +900,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   s.cval[lane] =
       (uint32_t)bush_value_fast(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1), p.bush_power);
   lds_publish(s.flag);  // every lane: each orders its own cval entry
-  __builtin_amdgcn_s_setprio(0);
+  WAB_PRIO(ROLL, 0);
   if (p.features && !p.restrict_view)  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
   SMALL_STAMP(11);
@@ -736,7 +908,9 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   SMALL_STAMP(12);
   lds_barrier();  // B1
   const uint32_t info = s.info[lane];
-  const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), s.kill[lane] != 0u);
+  const bool killed = s.kill[lane] != 0u;
+  const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), killed);
+  if (ROLL && !last) prefetch_actions(p, s, lane);  // the next step's (in LDS by the step's end)
   // the reset draws of the done envs for view cells [0, 64); W3 draws the rest and waits for
   // flag[1] before it builds the new episodes
   const unsigned long long jm = __ballot(job);
@@ -761,12 +935,23 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(14);
+  if (ROLL && lane == 0) {  // every hand-off of this step is done: clear the flags for the next
+    s.flag[0] = 0u;
+    s.flag[1] = 0u;
+    s.flag[2] = 0u;
+  }
+  if (ROLL && !last) {
+    const uint32_t status = info_starved(info) ? 1u : killed ? 2u : misc_status(h.hdr.z);
+    carry->hdr = job ? new_header(carry_of(s, lane), h)
+                     : make_uint4(h.cpos, (uint32_t)h.turn, misc_pack((uint32_t)h.role, status, 0u, 0u, 0u), h.hdr.w);
+  }
   return jm;
 }
 
 // --------------------------------------------------------------------------- W2: wolves
-template <int SLOTS, int G>
-__device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+template <int SLOTS, int G, bool ROLL = false>
+__device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane,
+                                                          CarryW2<SLOTS>* carry = nullptr, int t = 0, bool last = true) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   const bool active = g < p.B;
@@ -778,25 +963,36 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   uint32_t wr[SLOTS];
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
+  HeadRaw hr;
+  const bool carried = ROLL && t > 0;  // (multi-step launch: slots and mask from the last step)
+  if (carried) {
+    hr.hdr = carry->hdr;
+    hr.a = act_of(s, lane);
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) wr[k] = carry->wr[k];
+  } else {
   {
     const int64_t gl = active ? g : 0;  // (unconditional; an inactive lane has no live wolf)
 #pragma unroll
     for (int k = 0; k < kSpecSlots; ++k) wr[k] = p.wolves[(int64_t)k * p.B + gl];  // speculatively
   }
-  HeadRaw hr = head_fetch(p, g, active);
+  hr = head_fetch(p, g, active);
   opaque_head(hr);
 #pragma unroll
   for (int k = 0; k < kSpecSlots; ++k) opaque(wr[k]);
+  }
   const Head h = head_decode(p, g, active, hr);
-  lds_barrier();  // B_init
+  if (!ROLL || t == 0) lds_barrier();  // B_init
   SMALL_STAMP(28);
   const int nw = (int)misc_nw(h.hdr.z);
+  if (!carried) {
 #pragma unroll
-  for (int k = kSpecSlots; k < SLOTS; ++k)
-    if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
+    for (int k = kSpecSlots; k < SLOTS; ++k)
+      if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
+  }
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
   const uint32_t b0 = (uint32_t)ek, b1 = (uint32_t)(ek >> 32);
-  uint32_t live = nw >= 32 ? ~0u : ((1u << nw) - 1u);
+  uint32_t live = carried ? (h.active ? carry->live : 0u) : nw >= 32 ? ~0u : ((1u << nw) - 1u);
 
   // despawn (:262-264): one draw per wolf, keyed by its tile and its occurrence index among
   // the co-located wolves before it; groups of 4 slots, skipped when no lane has a wolf there
@@ -896,7 +1092,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   }
   // the next state of a continuing env: wolf slots and header (a done env's come from its
   // new episode)
-  if (active && !job) {
+  if (active && !job && (!ROLL || last)) {
     int n = 0;
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k)
@@ -913,16 +1109,49 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(20);
+  if (ROLL && !last) {  // the slots for the next step: a new episode's wolves from W3's cells
+    if (job) {
+      const NewEp n = carry_of(s, lane);
+      M128 m = n.wolves;
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) {
+        const bool any = (m.lo | m.hi) != 0ull;
+        const uint32_t c = m.lo ? (uint32_t)(__ffsll((unsigned long long)m.lo) - 1)
+                                : (uint32_t)(__ffsll((unsigned long long)m.hi) + 63);
+        carry->wr[k] = any ? s.tiles[any ? c : 0u] : 0u;
+        if (any) m_clear(m, c);
+      }
+      carry->live = n.nw >= 32u ? ~0u : ((1u << n.nw) - 1u);
+      carry->hdr = new_header(n, h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) carry->wr[k] = wr[k];
+      carry->live = live;
+      const uint32_t status = starved ? 1u : kill ? 2u : misc_status(h.hdr.z);
+      carry->hdr = make_uint4(h.cpos, (uint32_t)h.turn,
+                              misc_pack((info >> 8) & 0xFFu, status, (uint32_t)__popc(live), (info >> 16) & 0xFFu,
+                                        info >> 24),
+                              h.hdr.w);
+    }
+  }
   return jm;
 }
 
 // --------------------------------------------------------------------------- W3: ring
-template <int SLOTS, int G>
-__device__ __forceinline__ unsigned long long ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane) {
+template <int SLOTS, int G, bool ROLL = false>
+__device__ __forceinline__ unsigned long long ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane,
+                                                        CarryHdr* carry = nullptr, int t = 0, bool last = true) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
-  HeadRaw hr = head_fetch(p, g, g < p.B);
+  if (ROLL && WAB_ROLL_PRIO == 1) __builtin_amdgcn_s_setprio(0);  // (raised after B1 of the last step)
+  HeadRaw hr;
+  if (ROLL && t > 0) {  // (multi-step launch: the tables are in LDS since step 0)
+    hr.hdr = carry->hdr;
+    hr.a = act_of(s, lane);
+    reinterpret_cast<uint4*>(s.jbm)[lane] = make_uint4(0u, 0u, 0u, 0u);  // reset bitmaps [64][4]
+  } else {
+  hr = head_fetch(p, g, g < p.B);
   if constexpr (G == 11) {  // view-cell offsets (cw - i, ch - j) of cell c = 11 i + j, computed
     for (int c = lane; c < 121; c += 64) s.tiles[c] = xy_pack(5 - c / 11, 5 - c % 11);
   } else {
@@ -946,12 +1175,13 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
     for (int k = 0; k < 3; ++k)
       if (64 * k + lane < n) s.gap[64 * k + lane] = gv[k];
   }
+  }
   if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned)
     uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
     for (uint32_t i = lane; i < L.fzero / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const Head h = head_decode(p, g, g < p.B, hr);
-  lds_barrier();  // B_init
+  if (!ROLL || t == 0) lds_barrier();  // B_init
   if (p.features) {
     feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
     if (!p.restrict_view)  // rows 32..63 (step_features)
@@ -967,11 +1197,12 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   s.strip[64 + lane] = strip_draws(p, h, b0, b1, kStripW1, 1 << 30);  // the entering strip, part 2
   SMALL_STAMP(23);
   lds_barrier();  // B1
-  if constexpr (WAB_P1_PRIO) __builtin_amdgcn_s_setprio(3);
+  if constexpr (WAB_P1_PRIO) WAB_PRIO(ROLL, 3);
   // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
   // (unless the terminal obs is asked for: W0 after B2) the new episodes themselves
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(s.info[lane]), s.kill[lane] != 0u);
   const unsigned long long jm = __ballot(job);
+  int role2 = 0;
   if (jm) {
     const int j = __popcll(jm & ((1ull << lane) - 1ull));
     uint32_t* jkey = s.jkey + 2 * 64;  // this wave's copy of the keys
@@ -988,11 +1219,10 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
       // the part of the new episode that needs only its key, while W1 may still be drawing
       unsigned long long wolf_of = 0;
       const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB;
-      int role2 = 0;
-      if (job) role2 = new_episode_a<SLOTS>(p, s, h, g, (uint32_t)ek2, (uint32_t)(ek2 >> 32), ebit, wolf_of);
+      if (job) role2 = new_episode_a<SLOTS, ROLL>(p, s, h, g, (uint32_t)ek2, (uint32_t)(ek2 >> 32), ebit, wolf_of, last);
       lds_await(p, &s.flag[1]);  // W1's part of the draws
       SMALL_STAMP(9);
-      if (job) new_episode_b(p, s, g, j, ebit, role2);
+      if (job) new_episode_b(p, s, g, j, ebit, role2, !ROLL || last);
       if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     }
   }
@@ -1000,12 +1230,18 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(26);
+  if (ROLL && !last) {
+    const uint32_t status = info_starved(s.info[lane]) ? 1u : s.kill[lane] != 0u ? 2u : misc_status(h.hdr.z);
+    carry->hdr = job ? new_header(carry_of(s, lane), h)
+                     : make_uint4(h.cpos, (uint32_t)h.turn, misc_pack((uint32_t)h.role, status, 0u, 0u, 0u), h.hdr.w);
+  }
   return jm;
 }
 
 // --------------------------------------------------------------------------- obs stores
 // expand the 64-env bit-stream and store it with 16-byte stores, all 256 threads
-__device__ __forceinline__ void store_obs(const Params& p, const uint32_t* stream, int tid) {
+template <bool CLEAR = false>
+__device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int tid) {
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const uint32_t OB = (uint32_t)p.OB;
   const uint32_t limit = (uint32_t)min((int64_t)64, p.B - g0) * OB;
@@ -1020,6 +1256,14 @@ __device__ __forceinline__ void store_obs(const Params& p, const uint32_t* strea
   for (int k = 0; k < 6; ++k) {
     const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
     v[k] = u < full ? (uint32_t)s16[u] : 0u;
+  }
+  if constexpr (CLEAR) {  // (multi-step launches: each unit cleared by the thread that read it)
+    uint16_t* w16 = reinterpret_cast<uint16_t*>(stream);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
+      if (u < full) w16[u] = 0;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -1162,28 +1406,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     if constexpr (FEAT) step_features(p, L, lds, wave, lane);
   } else {
     // wab_rollout: n_steps steps of this group, one after the other (the envs of a workgroup
-    // depend on nothing outside it); the state goes through HBM as between launches, every
-    // store of step t complete (vmcnt) before step t + 1 reads it
-    for (int t = 0; t < p0.n_steps; ++t) {
-      if (t > 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+    // depend on nothing outside it), each wave's state carried in registers from step to step
+    // (see CarryW0): one barrier closes a step (its LDS is reused by the next)
+    const int T = p0.n_steps;
+    if (wave == 0) {
+      CarryW0 c;
+      for (int t = 0; t < T; ++t) {
+        Params p = wave_params<G, false>(p0);
+        step_slice(p, t);
+        const SmallLayout L = small_layout(p);
+        WAB_PRIO(true, 3);
+        bushes_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
+        WAB_PRIO(true, 0);
+        store_obs<true>(p, lds + L.stream, threadIdx.x);
+        lds_barrier();
       }
-      Params p = wave_params<G, false>(p0);
-      step_slice(p, t);
-      const SmallLayout L = small_layout(p);
-      if (wave == 0) {
-        __builtin_amdgcn_s_setprio(3);
-        bushes_wave<SLOTS, G>(p, L, lds, lane);
-        __builtin_amdgcn_s_setprio(0);
-      } else if (wave == 1) {
-        draws_wave<G>(p, L, lds, lane);
-      } else if (wave == 2) {
-        wolves_wave<SLOTS, G>(p, L, lds, lane);
-      } else {
-        ring_wave<SLOTS, G>(p, L, lds, lane);
+    } else if (wave == 1) {
+      CarryHdr c;
+      for (int t = 0; t < T; ++t) {
+        Params p = wave_params<G, false>(p0);
+        step_slice(p, t);
+        const SmallLayout L = small_layout(p);
+        draws_wave<G, true>(p, L, lds, lane, &c, t, t == T - 1);
+        store_obs<true>(p, lds + L.stream, threadIdx.x);
+        lds_barrier();
       }
-      store_obs(p, lds + L.stream, threadIdx.x);
+    } else if (wave == 2) {
+      CarryW2<SLOTS> c;
+      for (int t = 0; t < T; ++t) {
+        Params p = wave_params<G, false>(p0);
+        step_slice(p, t);
+        const SmallLayout L = small_layout(p);
+        wolves_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
+        store_obs<true>(p, lds + L.stream, threadIdx.x);
+        lds_barrier();
+      }
+    } else {
+      CarryHdr c;
+      for (int t = 0; t < T; ++t) {
+        Params p = wave_params<G, false>(p0);
+        step_slice(p, t);
+        const SmallLayout L = small_layout(p);
+        ring_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
+        store_obs<true>(p, lds + L.stream, threadIdx.x);
+        lds_barrier();
+      }
     }
   }
 }
