@@ -47,6 +47,7 @@ CONFIGS = {
                      "PragmaticObsWrapper features + discounted returns every %d steps, random policy"),
 }
 C5_SEGMENT = 32  # rollout segment length T (actor_critic.py collects one episode, <= 80 steps)
+DEFAULT_ROLLOUT = 32  # steps per wab_rollout launch of the default config's line
 
 
 def committed_traffic(config, batch):
@@ -62,6 +63,13 @@ def committed_traffic(config, batch):
 def alg_bytes_per_env_step(W, H):
     """1 B action + 3*W*H u8 obs + 8 B scalars/reward/done + 2*36 B state."""
     return 3 * W * H + 81
+
+
+def alg_bytes_per_env_step_rollout(W, H, T):
+    """A T-step rollout launch: per env-step the action, obs, scalars, reward and done
+    (3*W*H + 9 B); the 2*36 B of minimal state once per launch (read by the first step,
+    written by the last), i.e. 72 / T per env-step."""
+    return 3 * W * H + 9 + 72.0 / T
 
 
 def featurize_alg_bytes(W, H, F):
@@ -200,9 +208,11 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="graph", choices=["graph", "launch"])
-    ap.add_argument("--rollout", type=int, default=0,
+    ap.add_argument("--rollout", type=int, default=-1,
                     help="T > 0: wab_rollout segments of T steps (one launch each; obs, reward, done "
-                         "into a [T, B] rollout buffer) instead of one wab_step launch per step")
+                         "into a [T, B] rollout buffer) instead of one wab_step launch per step; "
+                         "0: per-step launches; default: %d for the default config (the small "
+                         "kernel's multi-step build), 0 otherwise" % DEFAULT_ROLLOUT)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
@@ -242,6 +252,10 @@ def main():
     opts, stride, slots, desc = CONFIGS[args.config]
     slots = args.wolf_slots or slots
     c5 = args.config == "c5"
+    if args.rollout < 0:
+        args.rollout = DEFAULT_ROLLOUT if args.config == "default" else 0
+    rollout = args.rollout > 0 and not c5
+    T_roll = args.rollout
     B, K, W = args.batch, args.steps, args.warmup
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
                                     env_id_base=env_id_base(rank, B),
@@ -253,7 +267,7 @@ def main():
         desc = desc % C5_SEGMENT
         K = max(C5_SEGMENT, K // C5_SEGMENT * C5_SEGMENT)  # whole segments
         W = max(C5_SEGMENT, -(-W // C5_SEGMENT) * C5_SEGMENT)
-    elif args.rollout > 0:
+    elif rollout:
         K = max(args.rollout, K // args.rollout * args.rollout)  # whole segments
         W = -(-W // args.rollout) * args.rollout
     env.reset()
@@ -295,7 +309,7 @@ def main():
                 if i == T - 1:
                     _lib.check(L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s),
                                "wab_discounted_returns_exact")
-    elif args.rollout > 0:
+    elif rollout:
         T = args.rollout
         seq_planes = torch.empty((T, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
         seq_scal = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
@@ -376,34 +390,50 @@ def main():
     kernel_name = "wab_step_%s (fused step)" % L.wab_step_kernel(h).decode()
     alg = alg_bytes_per_env_step(env.W, env.H)
     c5_line = None
-    if c5:
-        # C5 runs three kernels; each one's average launch comes from n back-to-back launches of
-        # that kernel alone, captured in a graph (as the timed region is) so that host launch
-        # cost does not pace a short kernel; HIP events on the launch stream around one replay
-        def per_launch(fn, n):
-            def launches(st):
-                sc = ctypes.c_void_p(st.cuda_stream)
-                for i in range(n):
-                    _lib.check(fn(i, sc), "c5 kernel timing")
-            if args.mode == "graph":
-                g = torch.cuda.CUDAGraph()
-                side = torch.cuda.Stream(dev)
-                side.wait_stream(stream)
-                with torch.cuda.stream(side):
-                    with torch.cuda.graph(g, stream=side):
-                        launches(torch.cuda.current_stream(dev))
-                stream.wait_stream(side)
-                g.replay()  # warm
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            if args.mode == "graph":
-                g.replay()
-            else:
-                launches(stream)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            return e0.elapsed_time(e1) / n
+    roll_line = None
 
+    # a kernel's average launch from n back-to-back launches of it alone, captured in a graph
+    # (as the timed region is) so that host launch cost does not pace a short kernel; HIP
+    # events on the launch stream around one replay
+    def per_launch(fn, n):
+        def launches(st):
+            sc = ctypes.c_void_p(st.cuda_stream)
+            for i in range(n):
+                _lib.check(fn(i, sc), "kernel timing")
+        if args.mode == "graph":
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(stream)
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    launches(torch.cuda.current_stream(dev))
+            stream.wait_stream(side)
+            g.replay()  # warm
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        if args.mode == "graph":
+            g.replay()
+        else:
+            launches(stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / n
+
+    if rollout:
+        # the gym surface's per-step launches (wab_step, obs into the same buffer each step),
+        # measured beside the rollout line; a rollout launch moves the state once per T steps
+        # (loaded by its first step, stored by its last), so its algorithmic bytes per env-step
+        # are the obs, action, scalars, reward and done plus 2 * 36 / T of state
+        ps_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), min(K, 512))
+        roll_line = {"steps_per_launch": T_roll, "launch_us": round(kern_ms * T_roll * 1e3, 3),
+                     "per_step_launch": {"api": "wab_step (BatchedWolvesAndBushesEnv.step)",
+                                         "us_per_step": round(ps_ms * 1e3, 3),
+                                         "env_steps_per_s": round(B / (ps_ms * 1e-3), 1),
+                                         "alg_bytes_per_env_step": alg,
+                                         "frac": round(alg * B / (ps_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+        alg = alg_bytes_per_env_step_rollout(env.W, env.H, T_roll)
+        kernel_name = "wab_step_%s, rollout build (%d steps per launch)" % (L.wab_step_kernel(h).decode(), T_roll)
+    if c5:
         n_k = min(K, 512)
         ret_ms = per_launch(lambda i, s: L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s), 64)
         if fused:
@@ -450,7 +480,8 @@ def main():
         achieved = achieved_rank
         value = world * B * K / elapsed
         # the committed PMC traffic is of the default launch of each config (C5: the fused one)
-        traffic, traffic_src = committed_traffic(args.config, B) if not args.c5_unfused else (None, None)
+        tkey = args.config + ("_rollout%d" % T_roll if rollout else "")
+        traffic, traffic_src = committed_traffic(tkey, B) if not args.c5_unfused else (None, None)
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -464,7 +495,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic: uniform random actions (torch.randint on device), keyed-RNG worlds",
-            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B * world,
+            "config": {"workload": desc + ("; %d-step wab_rollout launches (obs, reward, done of every "
+                                           "step into a [%d, B] rollout buffer)" % (T_roll, T_roll)
+                                           if rollout else "; one wab_step launch per step"),
+                       "batch_per_gpu": B, "global_batch": B * world,
                        "viewport": [Wv, Hv], "plane_stride": env.S, "wolf_slots": slots, "launch": args.mode,
                        "parallelism": "independent env shards x%d (no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -472,10 +506,10 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": alg * B,
+                         "alg_bytes_per_launch": round(alg * B * (T_roll if rollout else 1)),
                          "kernel": kernel_name,
-                         "kernel_us": round(kern_ms * 1e3, 3),
-                         "alg_bytes_per_env_step": alg},
+                         "kernel_us": round(kern_ms * 1e3 * (T_roll if rollout else 1), 3),
+                         "alg_bytes_per_env_step": round(alg, 3)},
             "stream_us_per_step": round(stream_ms * 1e3 / K, 3),
             "warmup_requested": args.warmup,
             "warmup_effective": W,
@@ -484,7 +518,7 @@ def main():
                          "eaten": counters["eaten_overflow"],
                          "handoff_timeouts": counters["handoff_timeouts"]},
         }
-        valu = committed_pmc(args.config, B) if not args.c5_unfused else None
+        valu = committed_pmc(tkey, B) if not args.c5_unfused else None
         if valu:
             line["roofline"]["valu"] = valu
         line["devices"] = sorted({r["pci"] for r in per_rank})
@@ -494,6 +528,10 @@ def main():
                 line["shared_gpus"] = True  # a rehearsal: ranks share a GPU, not a scaling figure
         if c5:
             line["c5"] = c5_line
+        if rollout:
+            line["rollout"] = roll_line
+        elif rollout:
+            line["rollout"]["per_step_launch"]["single_launch_median_us"] = round(single_ms * 1e3, 3)
         else:
             line["roofline"]["kernel_us_single_launch_median"] = round(single_ms * 1e3, 3)
         if world == 1 and not args.no_cpu:

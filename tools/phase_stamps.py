@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--lib", default=OUT, help="the stamps library to load (with --no-build)")
     ap.add_argument("--b2b", type=int, default=0,
                     help="instead: per-XCD entry/end of the last two of N back-to-back launches")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="instead: per-wave phases of the middle step of T-step wab_rollout launches")
     ap.add_argument("--graph", action="store_true",
                     help="with --b2b: the N launches captured in a graph and replayed (the bench's shape)")
     args = ap.parse_args()
@@ -59,6 +61,8 @@ def main():
     kind = env.step_kernel
     if args.b2b:
         return b2b_report(env, L, g, args.steps, args.b2b, args.graph)
+    if args.rollout:
+        return rollout_report(env, st, g, args.steps, args.rollout)
     if kind == "small":
         return small_report(env, st, g, args.steps)
     if kind == "wide":
@@ -222,6 +226,43 @@ def b2b_report(env, L, g, steps, n, graph=False):
     print("previous last end -> first entry (us):", us(gaps))
     if karg:
         print("entry -> first kernel-argument field by XCC (us):", us(karg))
+
+
+def rollout_report(env, st, g, launches, T):
+    """wab_rollout (the small kernel's multi-step build): the middle step's stamps of each wave
+    (SMALL_STAMP slots as in small_report; step t > 0 has no loads and no B_init), averaged over
+    workgroups and launches; times from the step's first stamp."""
+    import numpy as np
+    import torch
+
+    B = env.num_envs
+    nb = (B + 63) // 64
+    seqs = {"W0": [0, 1, 2, 7, 8, 3, 4, 5], "W1": [10, 30, 31, 11, 12, 13, 14],
+            "W2": [16, 28, 29, 17, 18, 19, 20], "W3": [22, 23, 24, 9, 25, 26]}
+    names = {"W0": ["start", "scroll", "-", "eaten log", "tile value", "eat/starve -> B1", "P1 -> B2", "after B2"],
+             "W1": ["start", "B_init", "key", "tile value", "strip", "P1 -> B2", "after B2"],
+             "W2": ["start", "B_init", "despawn", "pursuit/grid -> B1", "-", "P1 -> B2", "after B2"],
+             "W3": ["start", "spawn set + strip -> B1", "reset draws", "await W1", "new episodes -> B2", "after B2"]}
+    acc = {k: [] for k in seqs}
+    spans = []
+    for it in range(launches):
+        st.zero_()
+        a = torch.randint(0, env.n_actions, (T, B), device="cuda:0", generator=g).to(torch.int8)
+        env.rollout(a)
+        torch.cuda.synchronize()
+        if it < 3:
+            continue
+        s = st.cpu().numpy().astype(np.int64)[:nb]
+        t0 = s[:, [0, 10, 16, 22]].min(axis=1)
+        for k, cols in seqs.items():
+            v = s[:, cols]
+            ok = (v > 0).all(axis=1)
+            acc[k].append((v[ok] - t0[ok, None]).mean(axis=0))
+        spans.append((s[:, [5, 14, 20, 26]].max(axis=1) - t0).mean())
+    for k in seqs:
+        a = np.mean(acc[k], axis=0) * 10 / 1000
+        print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
+    print("step start -> last wave past B2 (mean over workgroups): %.2f us" % (np.mean(spans) * 10 / 1000))
 
 
 def small_report(env, st, g, steps):

@@ -157,6 +157,7 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) 
 struct SmallLayout {
   uint32_t tiles, thr, gap, stream, stream_words, cval, flag, wolfp, kill, bushp, strip, gone, info, spawn, jbm, jkey;
   uint32_t carry, act;  // multi-step launches: the new episodes' state for the next step, its actions
+  uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
 };
 
@@ -181,6 +182,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.jkey = o; o += 2u * 2u * 64u;
   L.carry = o; o += 8u * 64u;  // per env: role | new wolves << 8, food (2), wolf cells (4), pad
   L.act = o; o += 16u;         // 64 int8 actions
+  L.stream2 = o; o += L.stream_words + 4u;
   L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.fbits = L.ftab = L.fzero = L.scal = o;

@@ -45,7 +45,7 @@ namespace wab {
 #ifdef WAB_STAMPS
 #define SMALL_STAMP(slot)                                                                \
   do {                                                                                   \
-    if (lane == 0 && p.stamps)                                                           \
+    if (lane == 0 && p.stamps && (!ROLL || t == p.n_steps / 2))                          \
       p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 #else
@@ -427,6 +427,49 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
   }
 }
 
+// Multi-step launches (wab_rollout): NT threads (index idx) store NK units each (u = idx + NT
+// * k) of a finished step's stream into `planes` (that step's slice), clearing each unit after
+// its read so the stream can be rendered into again
+template <int NT, int NK>
+__device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes, uint32_t* stream, int idx) {
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const uint32_t OB = (uint32_t)p.OB;
+  const uint32_t full = ((uint32_t)min((int64_t)64, p.B - g0) * OB) >> 4;
+  uint8_t* out = planes + (size_t)g0 * OB;
+  uint16_t* s16 = reinterpret_cast<uint16_t*>(stream);
+  uint32_t v[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
+    v[k] = u < full ? (uint32_t)s16[u] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
+    if (u < full) s16[u] = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
+    if (u >= full) break;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 q;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+  }
+}
+
+// WAB_ROLL_STORE (A/B of the multi-step launch's obs stores): 0 every thread at the step's end
+// (one stream), 1 step t's by every thread half at the start and half at the end of step t + 1,
+// 2 step t's by W0 and W2 in their slack before B2 of step t + 1 (W1 and W3 never store)
+#ifndef WAB_ROLL_STORE
+#define WAB_ROLL_STORE 2
+#endif
+#ifndef WAB_ROLL_FLOOR  // diagnostic: skip every step's work, keep its obs stores
+#define WAB_ROLL_FLOOR 0
+#endif
+
 // --------------------------------------------------------------------------- multi-step launches
 // wab_rollout runs its T steps in one launch (ROLL): each wave keeps its part of an env's state
 // in registers from one step to the next (its view of the header; W0 also the food, the view
@@ -439,6 +482,8 @@ struct CarryHdr {
   uint4 hdr;  // the env's header at the start of the next step, as far as this wave uses it
 };
 struct CarryW0 {
+  uint8_t* prev_planes;   // the previous step's obs slice and stream (WAB_ROLL_STORE 2), or null
+  uint32_t* prev_stream;
   uint4 hdr;
   double food;
   uint32_t bw[4];            // view bitmap (post-eat)
@@ -446,9 +491,18 @@ struct CarryW0 {
 };
 template <int SLOTS>
 struct CarryW2 {
+  uint8_t* prev_planes;
+  uint32_t* prev_stream;
   uint4 hdr;
   uint32_t wr[SLOTS];  // wolf tiles, uncompacted
   uint32_t live;       // occupied slots
+};
+
+template <typename C>
+struct CarryPtr {  // (W1, W3: the loop's previous-step fields, unused by these waves)
+  uint8_t* prev_planes;
+  uint32_t* prev_stream;
+  C c;
 };
 
 __device__ __forceinline__ int act_of(const Lds& s, int lane) {
@@ -796,6 +850,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     lds_await(p, &s.flag[2]);  // S rendered (W2)
     store_units(p, s.stream, jm, false, 0, 3, lane);
   }
+  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
   SMALL_STAMP(4);
   lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
   if (p.t_planes) {
@@ -1105,6 +1160,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
   const unsigned long long jm = __ballot(job);
   if (early) store_units(p, s.stream, jm, false, 2, 3, lane);
+  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
   SMALL_STAMP(19);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -1240,6 +1296,41 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
 
 // --------------------------------------------------------------------------- obs stores
 // expand the 64-env bit-stream and store it with 16-byte stores, all 256 threads
+// Multi-step launches: units [K0, K1) of the six per thread of a finished step's stream (p its
+// step's slice), each cleared after its read so the stream can be rendered into again (steps
+// alternate between two streams, and step t's obs go out during step t + 1, half at its start
+// and half at its end, so that the obs stores do not all fall between two steps).  No
+// partial tail: a multi-step launch needs B * OB % 16 == 0 (wab_rollout).
+template <int K0, int K1>
+__device__ __forceinline__ void store_units_of(const Params& p, uint32_t* stream, int tid) {
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const uint32_t OB = (uint32_t)p.OB;
+  const uint32_t full = ((uint32_t)min((int64_t)64, p.B - g0) * OB) >> 4;
+  uint8_t* out = p.planes + (size_t)g0 * OB;
+  uint16_t* s16 = reinterpret_cast<uint16_t*>(stream);
+  uint32_t v[K1 - K0];
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
+    v[k - K0] = u < full ? (uint32_t)s16[u] : 0u;
+  }
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
+    if (u < full) s16[u] = 0;
+  }
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
+    if (u >= full) break;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 q;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) q[b] = (((v[k - K0] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+  }
+}
+
 template <bool CLEAR = false>
 __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int tid) {
   const int64_t g0 = (int64_t)blockIdx.x * 64;
@@ -1409,49 +1500,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     // depend on nothing outside it), each wave's state carried in registers from step to step
     // (see CarryW0): one barrier closes a step (its LDS is reused by the next)
     const int T = p0.n_steps;
+    {  // the second stream starts clear (the first is cleared by W0 in step 0)
+      const SmallLayout L = small_layout(p0);
+      uint4* z = reinterpret_cast<uint4*>(lds + L.stream2);
+      for (uint32_t i = threadIdx.x; i < L.stream_words / 4u; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    // one step of wave W's part; step t renders into stream t & 1 while step t - 1's obs go out
+    // (WAB_ROLL_STORE 1, 2; 0: one stream, stored at the step's end)
+#define WAB_ROLL_STEP(...)                                                                   \
+    for (int t = 0; t < T; ++t) {                                                            \
+      Params p = wave_params<G, false>(p0);                                                  \
+      step_slice(p, t);                                                                      \
+      const SmallLayout L0 = small_layout(p);                                                \
+      SmallLayout L = L0;                                                                    \
+      if (WAB_ROLL_STORE != 0 && (t & 1)) L.stream = L0.stream2;                             \
+      uint32_t* prev = lds + ((t & 1) ? L0.stream : L0.stream2);                             \
+      uint8_t* prev_planes = p.planes - (int64_t)p.B * p.OB;                                 \
+      c.prev_planes = prev_planes;                                                           \
+      c.prev_stream = (WAB_ROLL_STORE == 2 && t > 0) ? prev : nullptr;                       \
+      Params pp = p;                                                                         \
+      pp.planes = prev_planes;                                                               \
+      if (WAB_ROLL_STORE == 1 && t > 0) store_units_of<0, 3>(pp, prev, threadIdx.x);        \
+      if (WAB_ROLL_FLOOR) {  /* A/B floor: the stores alone (results wrong by design) */    \
+        lds_barrier();                                                                       \
+        lds_barrier();                                                                       \
+      } else {                                                                               \
+        __VA_ARGS__;                                                                         \
+      }                                                                                      \
+      if (WAB_ROLL_STORE == 1 && t > 0) store_units_of<3, 6>(pp, prev, threadIdx.x);        \
+      if (WAB_ROLL_STORE == 0) {                                                             \
+        store_obs<true>(p, lds + L.stream, threadIdx.x);                                     \
+      } else if (t == T - 1) {                                                               \
+        lds_barrier();                                                                       \
+        store_units_of<0, 6>(p, lds + L.stream, threadIdx.x);                                \
+      }                                                                                      \
+      lds_barrier();                                                                         \
+    }
     if (wave == 0) {
       CarryW0 c;
-      for (int t = 0; t < T; ++t) {
-        Params p = wave_params<G, false>(p0);
-        step_slice(p, t);
-        const SmallLayout L = small_layout(p);
+      WAB_ROLL_STEP({
         WAB_PRIO(true, 3);
         bushes_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
         WAB_PRIO(true, 0);
-        store_obs<true>(p, lds + L.stream, threadIdx.x);
-        lds_barrier();
-      }
+      })
     } else if (wave == 1) {
-      CarryHdr c;
-      for (int t = 0; t < T; ++t) {
-        Params p = wave_params<G, false>(p0);
-        step_slice(p, t);
-        const SmallLayout L = small_layout(p);
-        draws_wave<G, true>(p, L, lds, lane, &c, t, t == T - 1);
-        store_obs<true>(p, lds + L.stream, threadIdx.x);
-        lds_barrier();
-      }
+      CarryPtr<CarryHdr> c;
+      WAB_ROLL_STEP(draws_wave<G, true>(p, L, lds, lane, &c.c, t, t == T - 1))
     } else if (wave == 2) {
       CarryW2<SLOTS> c;
-      for (int t = 0; t < T; ++t) {
-        Params p = wave_params<G, false>(p0);
-        step_slice(p, t);
-        const SmallLayout L = small_layout(p);
-        wolves_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
-        store_obs<true>(p, lds + L.stream, threadIdx.x);
-        lds_barrier();
-      }
+      WAB_ROLL_STEP((wolves_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1)))
     } else {
-      CarryHdr c;
-      for (int t = 0; t < T; ++t) {
-        Params p = wave_params<G, false>(p0);
-        step_slice(p, t);
-        const SmallLayout L = small_layout(p);
-        ring_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
-        store_obs<true>(p, lds + L.stream, threadIdx.x);
-        lds_barrier();
-      }
+      CarryPtr<CarryHdr> c;
+      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1)))
     }
+#undef WAB_ROLL_STEP
   }
 }
 
