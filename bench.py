@@ -529,9 +529,8 @@ def main():
         if c5:
             line["c5"] = c5_line
         if rollout:
+            roll_line["per_step_launch"]["single_launch_median_us"] = round(single_ms * 1e3, 3)
             line["rollout"] = roll_line
-        elif rollout:
-            line["rollout"]["per_step_launch"]["single_launch_median_us"] = round(single_ms * 1e3, 3)
         else:
             line["roofline"]["kernel_us_single_launch_median"] = round(single_ms * 1e3, 3)
         if world == 1 and not args.no_cpu:
