@@ -39,12 +39,14 @@ CONFIGS = {
     # at 8 rows) live in HBM instead of being dropped
     "wide31": ({"width": 31, "height": 31}, 32, 32,
                "batch=65536 envs x 31x31 viewport in 32x32 planes (C3), random policy, autoreset"),
-    # C5: per step the step fused with the PragmaticObsWrapper features (wab_step_features) into
-    # a [T, B, 449] rollout buffer, reward/done straight into [T, B]; every T steps the
-    # discounted-return scan (wab_discounted_returns) over the segment (--c5-unfused: wab_step
-    # then wab_featurize)
+    # C5: T-step wab_rollout_features launches (the step fused with the PragmaticObsWrapper
+    # features into a [T, B, 449] rollout buffer, reward/done into [T, B], the segment's
+    # discounted returns at the launch's end); --rollout 0: one wab_step_features launch per step
+    # and the returns scan (wab_discounted_returns_exact) every T steps (--c5-unfused: wab_step
+    # then wab_featurize per step)
     "c5": ({}, 0, 8, "batch=65536 envs x default options, actor-critic rollout (C5): step + "
-                     "PragmaticObsWrapper features + discounted returns every %d steps, random policy"),
+                     "PragmaticObsWrapper features + discounted returns of each %d-step segment "
+                     "(episodes crossing a segment end are cut there, R_T = 0), random policy"),
 }
 C5_SEGMENT = 32  # rollout segment length T (actor_critic.py collects one episode, <= 80 steps)
 DEFAULT_ROLLOUT = 32  # steps per wab_rollout launch of the default config's line
@@ -70,6 +72,13 @@ def alg_bytes_per_env_step_rollout(W, H, T):
     (3*W*H + 9 B); the 2*36 B of minimal state once per launch (read by the first step,
     written by the last), i.e. 72 / T per env-step."""
     return 3 * W * H + 9 + 72.0 / T
+
+
+def c5_rollout_alg_bytes(F, T):
+    """A T-step wab_rollout_features launch per env-step: action, obs scalars, reward, done
+    (9 B), the F float32 features, the float32 return, and 72 / T of state (the planes are
+    rendered on chip and not stored)."""
+    return 9 + 4 * F + 4 + 72.0 / T
 
 
 def featurize_alg_bytes(W, H, F):
@@ -209,10 +218,11 @@ def main():
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="graph", choices=["graph", "launch"])
     ap.add_argument("--rollout", type=int, default=-1,
-                    help="T > 0: wab_rollout segments of T steps (one launch each; obs, reward, done "
-                         "into a [T, B] rollout buffer) instead of one wab_step launch per step; "
-                         "0: per-step launches; default: %d for the default config (the small "
-                         "kernel's multi-step build), 0 otherwise" % DEFAULT_ROLLOUT)
+                    help="T > 0: wab_rollout (c5: wab_rollout_features) segments of T steps (one "
+                         "launch each; obs or features, reward, done into a [T, B] rollout buffer) "
+                         "instead of one launch per step; 0: per-step launches; default: %d for the "
+                         "default config and c5 (the small kernel's multi-step build), 0 otherwise"
+                         % DEFAULT_ROLLOUT)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
@@ -253,7 +263,10 @@ def main():
     slots = args.wolf_slots or slots
     c5 = args.config == "c5"
     if args.rollout < 0:
-        args.rollout = DEFAULT_ROLLOUT if args.config == "default" else 0
+        args.rollout = DEFAULT_ROLLOUT if args.config in ("default", "c5") and not args.c5_unfused else 0
+    c5_roll = c5 and args.rollout > 0
+    if c5_roll:
+        args.rollout = C5_SEGMENT if args.rollout <= 0 else args.rollout
     rollout = args.rollout > 0 and not c5
     T_roll = args.rollout
     B, K, W = args.batch, args.steps, args.warmup
@@ -264,9 +277,10 @@ def main():
     # steady state: at least two full episodes' worth of untimed steps after the reset
     W = max(W, 2 * int(env.game_options["max_turns"]))
     if c5:
-        desc = desc % C5_SEGMENT
-        K = max(C5_SEGMENT, K // C5_SEGMENT * C5_SEGMENT)  # whole segments
-        W = max(C5_SEGMENT, -(-W // C5_SEGMENT) * C5_SEGMENT)
+        seg = T_roll if c5_roll else C5_SEGMENT
+        desc = desc % seg
+        K = max(seg, K // seg * seg)  # whole segments
+        W = max(seg, -(-W // seg) * seg)
     elif rollout:
         K = max(args.rollout, K // args.rollout * args.rollout)  # whole segments
         W = -(-W // args.rollout) * args.rollout
@@ -280,7 +294,7 @@ def main():
     a0 = actions.data_ptr()
     rew, done = env.reward.data_ptr(), env.done.data_ptr()
     if c5:
-        T = C5_SEGMENT
+        T = T_roll if c5_roll else C5_SEGMENT
         F = int(L.wab_feature_dim(h))
         feats = torch.empty((T, B, F), dtype=torch.float32, device=dev)
         seg_rew = torch.zeros((T, B), dtype=torch.float32, device=dev)
@@ -293,6 +307,9 @@ def main():
         o = env._obs["struct"]
         fobs = _lib.WabObs(None, o.food_turns, o.role, o.status)
         fobs_addr = ctypes.addressof(fobs)
+        seg_scal = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
+        rseq = _lib.WabObs(None, seg_scal[0].data_ptr(), seg_scal[1].data_ptr(), seg_scal[2].data_ptr())
+        rseq_addr = ctypes.addressof(rseq)
 
         def c5_step(t, i, s):
             if fused:
@@ -303,6 +320,11 @@ def main():
 
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
+            if c5_roll:  # one launch per segment: T fused steps and the segment's returns
+                for t in range(t0, t0 + n, T):
+                    _lib.check(L.wab_rollout_features(h, a0 + t * B, T, rseq_addr, r0, d0, f0, 0.99, None, ret0, s),
+                               "wab_rollout_features")
+                return
             for t in range(t0, t0 + n):
                 i = t % T
                 _lib.check(c5_step(t, i, s), "c5 step")
@@ -442,13 +464,24 @@ def main():
             # per env-step: the step's bytes without the planes (never stored), the F floats
             sf_alg = alg - 3 * env.W * env.H + 4 * F
             c5_line = {"segment": T, "feature_dim": F, "fused": True,
+                       "api": ("wab_rollout_features (%d steps + returns per launch)" % T if c5_roll else
+                               "wab_step_features per step + wab_discounted_returns_exact per segment"),
                        "step_features_us": round(sf_ms * 1e3, 3),
                        "returns_us_per_segment": round(ret_ms * 1e3, 3),
                        "returns_frac": round(RETURNS_ALG_BYTES * T * B / (ret_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                        "alg_bytes_per_env_step": sf_alg + RETURNS_ALG_BYTES,
                        "achieved_GBs_whole_step": round((sf_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
             kernel_name = "wab_step_%s + PragmaticObsWrapper features (wab_step_features)" % L.wab_step_kernel(h).decode()
-            alg, kern_ms = sf_alg, sf_ms
+            if c5_roll:
+                # the line's kernel is the rollout launch itself (kern_ms: per step from the
+                # timed region); the per-step fused launch is a diagnostic beside it
+                c5_line["rollout_launch_us"] = round(kern_ms * T * 1e3, 3)
+                c5_line["per_step_launch_frac"] = round(sf_alg * B / (sf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                alg = c5_rollout_alg_bytes(F, T)
+                kernel_name = ("wab_step_%s + PragmaticObsWrapper features + returns, rollout build (%d steps "
+                               "per launch, wab_rollout_features)" % (L.wab_step_kernel(h).decode(), T))
+            else:
+                alg, kern_ms = sf_alg, sf_ms
         step_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_k)
         feat_ms = per_launch(lambda i, s: L.wab_featurize(h, obs_addr, None, f0 + 4 * (i % T) * B * F, s), n_k)
         feat_alg = featurize_alg_bytes(env.W, env.H, F)
@@ -480,7 +513,7 @@ def main():
         achieved = achieved_rank
         value = world * B * K / elapsed
         # the committed PMC traffic is of the default launch of each config (C5: the fused one)
-        tkey = args.config + ("_rollout%d" % T_roll if rollout else "")
+        tkey = args.config + ("_rollout%d" % T_roll if rollout or c5_roll else "")
         traffic, traffic_src = committed_traffic(tkey, B) if not args.c5_unfused else (None, None)
         line = {
             "metric": METRIC,
@@ -497,7 +530,10 @@ def main():
             "data": "synthetic: uniform random actions (torch.randint on device), keyed-RNG worlds",
             "config": {"workload": desc + ("; %d-step wab_rollout launches (obs, reward, done of every "
                                            "step into a [%d, B] rollout buffer)" % (T_roll, T_roll)
-                                           if rollout else "; one wab_step launch per step"),
+                                           if rollout else
+                                           "; %d-step wab_rollout_features launches (features, reward, done, "
+                                           "returns into [%d, B] rollout buffers)" % (T_roll, T_roll)
+                                           if c5_roll else "; one step launch per step"),
                        "batch_per_gpu": B, "global_batch": B * world,
                        "viewport": [Wv, Hv], "plane_stride": env.S, "wolf_slots": slots, "launch": args.mode,
                        "parallelism": "independent env shards x%d (no collective)" % world},
@@ -506,9 +542,9 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": round(alg * B * (T_roll if rollout else 1)),
+                         "alg_bytes_per_launch": round(alg * B * (T_roll if rollout or c5_roll else 1)),
                          "kernel": kernel_name,
-                         "kernel_us": round(kern_ms * 1e3 * (T_roll if rollout else 1), 3),
+                         "kernel_us": round(kern_ms * 1e3 * (T_roll if rollout or c5_roll else 1), 3),
                          "alg_bytes_per_env_step": round(alg, 3)},
             "stream_us_per_step": round(stream_ms * 1e3 / K, 3),
             "warmup_requested": args.warmup,

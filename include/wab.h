@@ -24,6 +24,8 @@
  *   wab_featurize         <- PragmaticObsWrapper.observation         wab_env.py:726-824
  *   wab_featurize_superbasic <- SuperBasicObservationWrapper.observation wab_env.py:900-927
  *   wab_step_features        <- PragmaticObsWrapper(env).step, actor_critic.py:180-192
+ *   wab_rollout_features     <- T steps of actor_critic.main's loop     actor_critic.py:185-200
+ *                               + finish_episode's returns              actor_critic.py:139-143
  *   wab_render            <- WolvesAndBushesEnv.render (rgb_array,   wab_env.py:468-502
  *                            draw_health text included)
  *   wab_egocentric        <- WolvesAndBushesEnvEgoCentric._get_obs /  wab_env.py:930-979
@@ -42,7 +44,7 @@
 extern "C" {
 #endif
 
-#define WAB_ABI_VERSION 3
+#define WAB_ABI_VERSION 4
 #define WAB_MAX_WOLF_SLOTS 32 /* largest per-env live-wolf slot count (wab_config.wolf_slots) */
 #define WAB_MAX_VIEW 63       /* largest odd width/height accepted */
 
@@ -222,6 +224,21 @@ int wab_featurize(wab_handle* h, const wab_obs* obs, const uint8_t* view_mask, f
  * features (and planes, if set) must be 16-byte aligned. */
 int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward,
                       uint8_t* done, float* features, void* stream);
+
+/* T steps of PragmaticObsWrapper(WolvesAndBushesEnv).step with pre-chosen actions (the loop of
+ * actor_critic.main, actor_critic.py:185-200) and, if `returns` is non-NULL, the discounted
+ * returns of the segment (finish_episode, actor_critic.py:139-143): bit for bit T calls of
+ * wab_step_features (actions [T][B]; obs_seq scalars [T][B], planes [T][B][3][width][stride]
+ * or NULL; reward, done [T][B]; features [T][B][F]) followed by wab_discounted_returns_exact
+ * over the [T][B] reward/done (R_T = bootstrap[b], NULL = 0; returns [T][B] f32).  Where the
+ * fused small-view kernel steps the handle this is ONE launch: every workgroup takes its 64 envs
+ * through the T steps with the state in registers, step t's feature rows stored while step
+ * t + 1 runs, and (T <= 128) the returns computed from each step's exact double reward at the
+ * end; elsewhere T wab_step_features calls and wab_discounted_returns_exact.  Every step's
+ * features (and planes, if set) must be 16-byte aligned: B * F (B * OB) a multiple of 4 (16). */
+int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq,
+                         float* reward, uint8_t* done, float* features, double gamma,
+                         const float* bootstrap, float* returns, void* stream);
 
 /* SuperBasicObservationWrapper.observation (wab_env.py:900-927) + gym flatten: the nearest
  * bush of the bush grid (4 x Discrete(max_distance)), food, role, status -> one-hot float32

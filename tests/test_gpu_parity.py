@@ -715,3 +715,108 @@ def test_discounted_returns_exact_match_reference_finish_episode():
         last_done = np.nonzero(z["done"][idx[:, c]])[0][-1]
         np.testing.assert_allclose(norm[:last_done + 1, c], z["normalised32"][idx[:last_done + 1, c]],
                                    rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ config 5: fused rollout
+def _step_features_loop(env, a, F, store_planes):
+    """T step_features() calls of `env` (the unfused-launch reference of rollout_features)."""
+    import torch
+
+    T, B = a.shape
+    feats = torch.empty((T, B, F), device="cuda:0")
+    rew = torch.empty((T, B), device="cuda:0")
+    done = torch.empty((T, B), dtype=torch.uint8, device="cuda:0")
+    scal, planes = [], []
+    for t in range(T):
+        _, r, d = env.step_features(a[t], feats[t], store_planes=store_planes)
+        rew[t] = r
+        done[t] = d.to(torch.uint8)
+        scal.append(env._obs["scalars"].clone())
+        if store_planes:
+            planes.append(env._obs["planes"].clone())
+    return feats, rew, done, torch.stack(scal), (torch.stack(planes) if store_planes else None)
+
+
+@pytest.mark.parametrize("opts,kw,T,planes", [
+    (None, {}, 40, False),                                            # G = 11, 8 slots
+    (None, {}, 33, True),                                             # planes stored too
+    ({"width": 9, "height": 9, "starting_food": None, "starting_role": None}, {"wolf_slots": 16}, 40, False),
+    ({"restrict_view": True, "lookout_only": False}, {"wolf_slots": 32}, 40, False),
+    (None, {"autoreset": False}, 90, False),                          # stepping past done
+    (None, {}, 130, False),                                           # T > 128: returns by the scan kernel
+    ({"width": 9, "height": 13}, {}, 20, False),                      # not fusable: step_features loop
+])
+def test_rollout_features_equals_step_features_loop(opts, kw, T, planes):
+    """wab_rollout_features (one launch: T fused steps + the segment's returns) == T
+    wab_step_features calls + wab_discounted_returns_exact, bit for bit, over two consecutive
+    rollouts (state carried across calls; the second with a bootstrap), a partial last group
+    included; final hidden state and counters equal too."""
+    import torch
+
+    from wab_gym_amd.wrappers import discounted_returns
+
+    B = 1008  # 15 full groups + 48 envs; B * 449 (B * 363) a multiple of 4 (16): aligned steps
+    e1, e2 = _env(opts, B, validate_actions=False, **kw), _env(opts, B, validate_actions=False, **kw)
+    e1.reset()
+    e2.reset()
+    rs = np.random.RandomState(11)
+    for seg in range(2):
+        a = torch.as_tensor(rs.randint(e1.n_actions, size=(T, B)))
+        bs = None if seg == 0 else torch.as_tensor(rs.standard_normal(B).astype(np.float32), device="cuda:0")
+        r = e1.rollout_features(a, gamma=0.97, bootstrap=bs, store_planes=planes)
+        F = r["features"].shape[2]
+        feats, rew, done, scal, pl = _step_features_loop(e2, a.cuda(), F, planes)
+        for t in range(T):
+            assert torch.equal(r["features"][t], feats[t]), (seg, t)
+            assert torch.equal(r["scalars"][t], scal[t]), (seg, t)
+        assert torch.equal(r["reward"], rew) and torch.equal(r["done"], done), seg
+        if planes:
+            assert torch.equal(r["planes"], pl), seg
+        want = discounted_returns(rew, done, gamma=0.97, bootstrap=bs, env=e2)
+        assert torch.equal(r["returns"], want), seg
+    s1, s2 = e1.state(), e2.state()
+    for k in s1:
+        assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
+    assert e1.counters() == e2.counters()
+
+
+def test_rollout_features_full_size_c5():
+    """C5 at full size (B = 65536, T = 32, the bench's segment): the single rollout launch ==
+    32 fused step launches + the exact returns scan, bit for bit, twice in a row; the returns
+    equal the reference's recursion run in float64 on the host for a sample of envs."""
+    import torch
+
+    from wab_gym_amd.wrappers import discounted_returns
+
+    B, T = 65536, 32
+    e1, e2 = _env(None, B, validate_actions=False), _env(None, B, validate_actions=False)
+    e1.reset()
+    e2.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(21)
+    for seg in range(2):
+        a = torch.randint(0, 5, (T, B), device="cuda:0", generator=g).to(torch.int8)
+        r = e1.rollout_features(a)
+        feats, rew, done, scal, _ = _step_features_loop(e2, a, 449, False)
+        assert torch.equal(r["features"], feats), seg
+        assert torch.equal(r["reward"], rew) and torch.equal(r["done"], done), seg
+        assert torch.equal(r["scalars"], scal), seg
+        assert torch.equal(r["returns"], discounted_returns(rew, done, gamma=0.99, env=e2)), seg
+        del feats
+    # finish_episode's loop (actor_critic.py:139-143) on the float64 rewards of 64 envs
+    opts = e1.game_options
+    rt = rew.double().cpu().numpy()
+    dn = done.cpu().numpy()
+    exact = {np.float32(v): v for v in (opts["reward_per_turn"], opts["reward_for_finishing"],
+                                        opts["reward_for_starving"], opts["reward_for_being_killed"])}
+    for x in list(exact.values()):
+        exact[np.float32(0.0 + opts["reward_for_eating"] + x)] = 0.0 + opts["reward_for_eating"] + x
+    ret = r["returns"].cpu().numpy()
+    for b in range(0, B, B // 64):
+        R = 0.0
+        for t in range(T - 1, -1, -1):
+            if dn[t, b]:
+                R = 0.0
+            R = exact.get(np.float32(rt[t, b]), float(rt[t, b])) + 0.99 * R
+            assert np.float32(R) == ret[t, b], (b, t)
+    assert e1.counters() == e2.counters()

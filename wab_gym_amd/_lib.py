@@ -18,10 +18,10 @@ EXPORTED = [
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
     "wab_debug_bush_values", "wab_step_features", "wab_discounted_returns_exact",
-    "wab_bush_thresholds",
+    "wab_bush_thresholds", "wab_rollout_features",
 ]
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class WabObs(ctypes.Structure):
@@ -78,6 +78,7 @@ def load():
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_discounted_returns_exact.argtypes = [P, P, P, I32, I64, ctypes.c_double, P, P, P]
     L.wab_bush_thresholds.argtypes = [ctypes.c_double, I32, P]
+    L.wab_rollout_features.argtypes = [P, P, I32, P, P, P, P, ctypes.c_double, P, P, P]
     L.wab_batch.argtypes = [P]
     L.wab_batch.restype = I64
     L.wab_step_kernel.argtypes = [P]

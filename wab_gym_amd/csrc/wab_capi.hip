@@ -169,9 +169,9 @@ void* small_kernel_ptr(int slots) {
 
 // ROLL: the multi-step build (Params::n_steps steps per launch, wab_rollout)
 template <int G, bool FEAT = false, bool ROLL = false>
-void launch_small(wab_handle* h, const Params& p, hipStream_t stream) {
+void launch_small(wab_handle* h, const Params& p, hipStream_t stream, size_t lds_bytes = 0) {
   const dim3 grid(h->n_blocks), block(256);  // one 64-env group per workgroup, four waves
-  const size_t lds = FEAT ? h->small_feat_lds_bytes : h->small_lds_bytes;
+  const size_t lds = lds_bytes ? lds_bytes : FEAT ? h->small_feat_lds_bytes : h->small_lds_bytes;
   switch (h->slots) {
     case 8: hipLaunchKernelGGL((wab::wab_step_small<8, G, FEAT, ROLL>), grid, block, lds, stream, p); break;
     case 16: hipLaunchKernelGGL((wab::wab_step_small<16, G, FEAT, ROLL>), grid, block, lds, stream, p); break;
@@ -869,6 +869,68 @@ int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, 
   else launch_small<0, true>(h, p, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return WAB_OK;
+}
+
+int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq, float* reward,
+                         uint8_t* done, float* features, double gamma, const float* bootstrap, float* returns,
+                         void* stream) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_rollout_features: NULL handle");
+  if (T < 0) return fail(WAB_E_INVALID, "wab_rollout_features: T must be >= 0");
+  if (!h->reset_done) return fail(WAB_E_STATE, "wab_rollout_features: call wab_reset before the first step");
+  if (!actions || !reward || !done || !features || !obs_seq || !obs_seq->food_turns || !obs_seq->role ||
+      !obs_seq->status)
+    return fail(WAB_E_INVALID, "wab_rollout_features: NULL argument");
+  const int F = wab_feature_dim(h);
+  if (F < 0) return fail(WAB_E_INVALID, "wab_rollout_features: the wrapper cannot index this viewport");
+  const int64_t B = h->p.B;
+  const size_t OB = (size_t)h->p.OB;
+  if (!aligned16(features) || (T > 1 && ((size_t)B * (size_t)F * 4u) % 16u != 0))
+    return fail(WAB_E_INVALID, "wab_rollout_features: every step's features must be 16-byte aligned "
+                               "(features aligned, batch * feature_dim a multiple of 4)");
+  if (obs_seq->planes && (!aligned16(obs_seq->planes) || (T > 1 && ((size_t)B * OB) % 16u != 0)))
+    return fail(WAB_E_INVALID, "wab_rollout_features: every step's planes must be 16-byte aligned");
+  if (T == 0 || B == 0) return WAB_OK;
+  const bool fused_returns = returns && T <= wab::kMaxFusedReturnSteps;
+  if (h->small_feat_lds_bytes && h->step_kernel == KERNEL_SMALL) {
+    // one launch: each workgroup runs its 64 envs through the T steps with the featurizer fused
+    // (wab_step_small<.., FEAT, ROLL>), the returns of the segment at its end
+    Params p = h->p;
+    p.actions = actions;
+    p.planes = obs_seq->planes;
+    p.food_turns = obs_seq->food_turns;
+    p.role = obs_seq->role;
+    p.status = obs_seq->status;
+    p.reward = reward;
+    p.done = done;
+    p.features = features;
+    p.n_steps = T;
+    if (fused_returns) {
+      p.returns = returns;
+      p.bootstrap = bootstrap;
+      p.gamma = gamma;
+    }
+    const size_t lds = (size_t)wab::small_layout(p).total * 4u;
+    DeviceGuard guard(h->device);
+    if (h->small_g11) launch_small<11, true, true>(h, p, (hipStream_t)stream, lds);
+    else launch_small<0, true, true>(h, p, (hipStream_t)stream, lds);
+    HIP_TRY(hipGetLastError());
+    if (fused_returns) return WAB_OK;
+  } else {
+    for (int32_t t = 0; t < T; ++t) {  // (no fused kernel for these options: T fused-or-not steps)
+      wab_obs o;
+      o.planes = obs_seq->planes ? obs_seq->planes + (size_t)t * (size_t)B * OB : nullptr;
+      o.food_turns = obs_seq->food_turns + (size_t)t * (size_t)B;
+      o.role = obs_seq->role + (size_t)t * (size_t)B;
+      o.status = obs_seq->status + (size_t)t * (size_t)B;
+      int rc = wab_step_features(h, actions + (size_t)t * (size_t)B, &o, reward + (size_t)t * (size_t)B,
+                                 done + (size_t)t * (size_t)B, features + (size_t)t * (size_t)B * (size_t)F,
+                                 stream);
+      if (rc != WAB_OK) return rc;
+    }
+  }
+  if (!returns) return WAB_OK;
+  return wab_discounted_returns_exact(h, reward, done, T, B, gamma, bootstrap, returns, stream);
 }
 
 int wab_superbasic_dim(const wab_handle* h) {

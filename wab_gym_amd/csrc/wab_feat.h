@@ -140,6 +140,14 @@ __device__ __forceinline__ void emit_scalars(uint32_t* ob, uint32_t at, int md, 
 // float4s u = t + nthreads * i (consecutive lanes, consecutive 16 bytes), i.e. the nibbles at
 // bit 4 (t & 7) of dwords (t >> 3) + (nthreads / 8) i: one LDS read and four bit-field
 // extracts and conversions per float4 (nthreads a multiple of 8)
+__device__ __forceinline__ void nt_store_f4(const float4& f, float4* dst) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const f32x4 v = {f.x, f.y, f.z, f.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+}
+
+// (NT: non-temporal stores)
+template <bool NT = false>
 __device__ __forceinline__ void store_feature_bits(const uint32_t* ob, float* out, uint32_t nf, int tid, int nthreads) {
   const uint32_t nq = nf >> 2, sh = 4u * ((uint32_t)tid & 7u), step = (uint32_t)nthreads >> 3;
   const uint32_t* src = ob + ((uint32_t)tid >> 3);
@@ -153,7 +161,8 @@ __device__ __forceinline__ void store_feature_bits(const uint32_t* ob, float* ou
     f.y = (float)__builtin_amdgcn_ubfe(w, sh + 1u, 1u);
     f.z = (float)__builtin_amdgcn_ubfe(w, sh + 2u, 1u);
     f.w = (float)__builtin_amdgcn_ubfe(w, sh + 3u, 1u);
-    dst[(size_t)nthreads * i] = f;
+    if (NT) nt_store_f4(f, dst + (size_t)nthreads * i);
+    else dst[(size_t)nthreads * i] = f;
   }
   for (uint32_t q = 4u * nq + (uint32_t)tid; q < nf; q += (uint32_t)nthreads)
     out[q] = ((ob[q >> 5] >> (q & 31u)) & 1u) ? 1.0f : 0.0f;
@@ -200,6 +209,7 @@ __device__ __forceinline__ void view_zero_lines(float* out, uint32_t F, uint32_t
 }
 
 // store_feature_bits without the chunks in the whole view-block lines (view_zero_lines)
+template <bool NT = false>
 __device__ __forceinline__ void store_rows_skip_views(const uint32_t* ob, float* out, uint32_t nf, uint32_t F, int tid,
                                                       int nthreads) {
   const ViewLines v = view_lines(out, F);
@@ -220,7 +230,8 @@ __device__ __forceinline__ void store_rows_skip_views(const uint32_t* ob, float*
       f.y = (float)__builtin_amdgcn_ubfe(w, sh + 1u, 1u);
       f.z = (float)__builtin_amdgcn_ubfe(w, sh + 2u, 1u);
       f.w = (float)__builtin_amdgcn_ubfe(w, sh + 3u, 1u);
-      reinterpret_cast<float4*>(out)[u] = f;
+      if (NT) nt_store_f4(f, reinterpret_cast<float4*>(out) + u);
+      else reinterpret_cast<float4*>(out)[u] = f;
     }
     e += dq;
     r += dr;

@@ -121,6 +121,9 @@ struct Params {
   uint8_t* t_role;
   uint8_t* t_status;
   float* features;     // wab_step_features: PragmaticObsWrapper features [B][F] (else null)
+  float* returns;      // wab_rollout_features: discounted returns [n_steps][B] (else null)
+  const float* bootstrap;  // ... R after the last step [B] (null: 0)
+  double gamma;
   unsigned long long* stamps;  // diagnostic builds only (-DWAB_STAMPS): [n_blocks][40] s_memrealtime
 };
 
@@ -152,6 +155,10 @@ __host__ __device__ inline LdsLayout lds_layout(const Params& p, int /*slots*/) 
   return L;
 }
 
+// wab_rollout_features computes the returns in the kernel for segments of at most this many
+// steps (their reward codes in LDS); longer ones run wab_discounted_returns_exact after it
+constexpr int kMaxFusedReturnSteps = 128;
+
 // LDS of the four-wave small-view step (wab_step_small.hip): one 64-env group per
 // workgroup (dwords)
 struct SmallLayout {
@@ -159,6 +166,7 @@ struct SmallLayout {
   uint32_t carry, act;  // multi-step launches: the new episodes' state for the next step, its actions
   uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
+  uint32_t rcode;       // wab_rollout_features with returns: [n_steps][64] reward codes (bytes)
 };
 
 __host__ __device__ inline SmallLayout small_layout(const Params& p) {
@@ -195,6 +203,8 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
     L.fzero = o - L.fbits;
     L.scal = o; o += 64u;
   }
+  L.rcode = o;
+  if (p.returns) o += 16u * (uint32_t)p.n_steps;  // one byte per env and step
   L.total = o;
   return L;
 }

@@ -275,6 +275,7 @@ struct Lds {
   uint32_t* scal;   // [64] fused features: food_turns | role << 8 | status << 16 of the obs
   uint32_t* carry;  // [64][8] multi-step launches: a new episode's role | wolves << 8, food, wolf cells (W3)
   uint32_t* act;    // [16] multi-step launches: the next step's 64 actions (W1)
+  uint8_t* rcode;   // [n_steps][64] wab_rollout_features with returns: each step's reward code (W0)
 };
 
 __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
@@ -297,6 +298,7 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   s.scal = lds + L.scal;
   s.carry = lds + L.carry;
   s.act = lds + L.act;
+  s.rcode = reinterpret_cast<uint8_t*>(lds + L.rcode);
   return s;
 }
 
@@ -427,6 +429,10 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
   }
 }
 
+// multi-step launches: obs stores non-temporal (1) or plain (0) (A/B)
+#ifndef WAB_ROLL_NT
+#define WAB_ROLL_NT 1
+#endif
 // Multi-step launches (wab_rollout): NT threads (index idx) store NK units each (u = idx + NT
 // * k) of a finished step's stream into `planes` (that step's slice), clearing each unit after
 // its read so the stream can be rendered into again
@@ -448,6 +454,7 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
     const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
     if (u < full) s16[u] = 0;
   }
+  if (!planes) return;  // (wab_rollout_features without planes: the stream is only cleared)
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
@@ -456,7 +463,8 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
     u32x4 q;
 #pragma unroll
     for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    if (WAB_ROLL_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    else reinterpret_cast<u32x4*>(out)[u] = q;
   }
 }
 
@@ -621,6 +629,12 @@ __device__ __forceinline__ void new_episode_b(const Params& p, const Lds& s, int
   if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(nbm);
 }
 
+// multi-step launches: the view-mask zero lines stored early in each step (1) or with the rest
+// of the rows (0) (A/B)
+#ifndef WAB_ROLL_EARLY_VIEWS
+#define WAB_ROLL_EARLY_VIEWS 1
+#endif
+
 // --------------------------------------------------------------------------- fused features: early lines
 // The view-mask blocks of the feature rows are all zeros without restrict_view, known before
 // the step has computed anything: the whole 128-byte lines inside them (wab_feat.h) are stored
@@ -629,6 +643,35 @@ __device__ __forceinline__ void new_episode_b(const Params& p, const Lds& s, int
 __device__ __forceinline__ void early_view_zeros(const Params& p, uint32_t e0, uint32_t n_rows, int lane) {
   const uint32_t F = (uint32_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
   view_zero_lines(p.features + (size_t)blockIdx.x * 64u * F, F, e0, n_rows, lane, 64);
+}
+
+// --------------------------------------------------------------------------- fused returns
+// wab_rollout_features: each step W0 keeps its env's reward as a code in LDS (ate, the outcome,
+// done), and after the last step runs finish_episode's scan over the launch's steps
+// (actor_critic.py:139-143: R = r + gamma R from the last step back, restarted after every
+// done, R_T = bootstrap or 0), in double from the reward's own terms, float32 out.  The same
+// doubles as wab_discounted_returns_exact recovers from the float32 rewards, so the two agree
+// bit for bit (and this one needs no unambiguous reward table).
+__device__ __forceinline__ uint8_t reward_code(bool ate, int status, bool done) {
+  const uint32_t outcome = status == 0 ? (done ? 1u : 0u) : status == 1 ? 2u : 3u;
+  return (uint8_t)((ate ? 1u : 0u) | (outcome << 1) | (done ? 8u : 0u));
+}
+
+__device__ __forceinline__ void rollout_returns(const Params& p, const Lds& s, int64_t g, bool active, int lane) {
+  if (!active) return;
+  const double r_eat = p.r_eat, gamma = p.gamma;
+  const double rx[4] = {p.r_turn, p.r_finish, p.r_starve, p.r_killed};
+  double R = p.bootstrap ? (double)p.bootstrap[g] : 0.0;
+  for (int t = p.n_steps - 1; t >= 0; --t) {
+    const uint32_t c = s.rcode[64 * t + lane];
+    const uint32_t o = (c >> 1) & 3u;
+    const double x = o == 0u ? rx[0] : o == 1u ? rx[1] : o == 2u ? rx[2] : rx[3];
+    // the step's reward as W0 summed it: 0 + r_eat (if it ate) + r_x (:299-340)
+    const double r = (c & 1u) ? (0.0 + r_eat) + x : 0.0 + x;
+    if (c & 8u) R = 0.0;
+    R = r + gamma * R;  // (no contraction: -ffp-contract=off)
+    p.returns[(int64_t)t * p.B + g] = (float)R;
+  }
 }
 
 // --------------------------------------------------------------------------- W0: bushes
@@ -765,7 +808,8 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   SMALL_STAMP(8);
   double reward = 0.0;
   unsigned long long eaten_of = 0;
-  if (rem > 0 && status_old == 0 && (role == 1 || p.lookout_only)) {  // eat (:299-313), stale status
+  const bool ate = rem > 0 && status_old == 0 && (role == 1 || p.lookout_only);
+  if (ate) {  // eat (:299-313), stale status
     food = food + p.fill;
     food = food < 0.0 ? 0.0 : (food > 1.0 ? 1.0 : food);
     reward += p.r_eat;
@@ -815,6 +859,8 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     reward += sel_f64(status == 0, sel_f64(done, r_finish, r_turn), sel_f64(status == 1, r_starve, r_killed));
   }
   const bool job = active && done && p.autoreset;
+  if (ROLL && p.returns)  // the step's reward as a code for the returns at the launch's end
+    s.rcode[64 * t + lane] = reward_code(ate, status, done);
   if (active) {
     const int ft = (int)ceil(food * (double)p.turns_empty);  // :450-452
     __builtin_nontemporal_store((float)reward, p.reward + g);
@@ -913,6 +959,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
         }
     }
   }
+  if (ROLL && last && p.returns) rollout_returns(p, s, g, active, lane);
   SMALL_STAMP(5);
   return jm;
 }
@@ -956,7 +1003,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
       (uint32_t)bush_value_fast(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1), p.bush_power);
   lds_publish(s.flag);  // every lane: each orders its own cval entry
   WAB_PRIO(ROLL, 0);
-  if (p.features && !p.restrict_view)  // rows 0..31 (step_features)
+  if (p.features && !p.restrict_view && (!ROLL || WAB_ROLL_EARLY_VIEWS))  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
   SMALL_STAMP(11);
   s.strip[lane] = strip_draws(p, h, b0, b1, 0, kStripW1);  // generate_bushes (:613-629): the entering strip
@@ -1232,15 +1279,18 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
       if (64 * k + lane < n) s.gap[64 * k + lane] = gv[k];
   }
   }
-  if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned)
+  if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned;
+                     // multi-step launches: the tables once, the bits every step)
     uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
-    for (uint32_t i = lane; i < L.fzero / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t nz = ROLL && t > 0 ? L.ftab - L.fbits : L.fzero;
+    for (uint32_t i = lane; i < nz / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const Head h = head_decode(p, g, g < p.B, hr);
   if (!ROLL || t == 0) lds_barrier();  // B_init
   if (p.features) {
-    feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
-    if (!p.restrict_view)  // rows 32..63 (step_features)
+    if (!ROLL || t == 0)
+      feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
+    if (!p.restrict_view && (!ROLL || WAB_ROLL_EARLY_VIEWS))  // rows 32..63 (step_features)
       early_view_zeros(p, 32u, (uint32_t)max((int64_t)0, min((int64_t)32, p.B - (int64_t)blockIdx.x * 64 - 32)), lane);
   }
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
@@ -1327,7 +1377,8 @@ __device__ __forceinline__ void store_units_of(const Params& p, uint32_t* stream
     u32x4 q;
 #pragma unroll
     for (int b = 0; b < 4; ++b) q[b] = (((v[k - K0] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    if (WAB_ROLL_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    else reinterpret_cast<u32x4*>(out)[u] = q;
   }
 }
 
@@ -1382,6 +1433,11 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
 // from the rendered bit-stream (after B2, or B3) and the scalars each env's writer handed over:
 // W0 the wolf plane, W1 the bush plane, W2 the scalars and view mask, one more barrier, then
 // all 256 threads expand the feature bits to float32 (the featurizer's phases 2 and 3).
+// multi-step launches: feature rows non-temporal (1) or plain (0) (A/B)
+#ifndef WAB_ROLL_FEAT_NT
+#define WAB_ROLL_FEAT_NT 0
+#endif
+template <bool ROLL = false>
 __device__ __forceinline__ void step_features(const Params& p, const SmallLayout& L, uint32_t* lds, int wave,
                                               int lane) {
   const int md = p.W / 2 + p.H / 2 + 1;
@@ -1407,8 +1463,9 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
     }
   }
   lds_barrier();
-  if (p.restrict_view) store_feature_bits(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
-  else store_rows_skip_views(ob, p.features + (size_t)g0 * F, n_active * F, F, (int)threadIdx.x, 256);
+  constexpr bool NT = ROLL && WAB_ROLL_FEAT_NT;
+  if (p.restrict_view || (ROLL && !WAB_ROLL_EARLY_VIEWS)) store_feature_bits<NT>(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
+  else store_rows_skip_views<NT>(ob, p.features + (size_t)g0 * F, n_active * F, F, (int)threadIdx.x, 256);
 }
 
 }  // namespace
@@ -1445,6 +1502,7 @@ __device__ __forceinline__ void step_slice(Params& p, int t) {
   p.status += o;
   p.reward += o;
   p.done += o;
+  if (p.features) p.features += o * pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
 }
 
 template <int SLOTS, int G, bool FEAT, bool ROLL>
@@ -1509,28 +1567,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     // (WAB_ROLL_STORE 1, 2; 0: one stream, stored at the step's end)
 #define WAB_ROLL_STEP(...)                                                                   \
     for (int t = 0; t < T; ++t) {                                                            \
-      Params p = wave_params<G, false>(p0);                                                  \
+      Params p = wave_params<G, FEAT>(p0);                                                   \
       step_slice(p, t);                                                                      \
       const SmallLayout L0 = small_layout(p);                                                \
       SmallLayout L = L0;                                                                    \
       if (WAB_ROLL_STORE != 0 && (t & 1)) L.stream = L0.stream2;                             \
       uint32_t* prev = lds + ((t & 1) ? L0.stream : L0.stream2);                             \
-      uint8_t* prev_planes = p.planes - (int64_t)p.B * p.OB;                                 \
+      uint8_t* prev_planes = p.planes ? p.planes - (int64_t)p.B * p.OB : nullptr;            \
       c.prev_planes = prev_planes;                                                           \
       c.prev_stream = (WAB_ROLL_STORE == 2 && t > 0) ? prev : nullptr;                       \
       Params pp = p;                                                                         \
       pp.planes = prev_planes;                                                               \
-      if (WAB_ROLL_STORE == 1 && t > 0) store_units_of<0, 3>(pp, prev, threadIdx.x);        \
+      if (WAB_ROLL_STORE == 1 && t > 0 && pp.planes) store_units_of<0, 3>(pp, prev, threadIdx.x); \
       if (WAB_ROLL_FLOOR) {  /* A/B floor: the stores alone (results wrong by design) */    \
         lds_barrier();                                                                       \
         lds_barrier();                                                                       \
       } else {                                                                               \
         __VA_ARGS__;                                                                         \
       }                                                                                      \
-      if (WAB_ROLL_STORE == 1 && t > 0) store_units_of<3, 6>(pp, prev, threadIdx.x);        \
+      if (FEAT) step_features<true>(p, L, lds, wave, lane);  /* this step's rows */        \
+      if (WAB_ROLL_STORE == 1 && t > 0 && pp.planes) store_units_of<3, 6>(pp, prev, threadIdx.x); \
       if (WAB_ROLL_STORE == 0) {                                                             \
-        store_obs<true>(p, lds + L.stream, threadIdx.x);                                     \
-      } else if (t == T - 1) {                                                               \
+        if (p.planes) store_obs<true>(p, lds + L.stream, threadIdx.x);                       \
+      } else if (t == T - 1 && p.planes) {                                                   \
         lds_barrier();                                                                       \
         store_units_of<0, 6>(p, lds + L.stream, threadIdx.x);                                \
       }                                                                                      \
@@ -1560,20 +1619,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
 template __global__ void wab_step_small<8, 0, false, false>(Params);
 template __global__ void wab_step_small<8, 0, true, false>(Params);
 template __global__ void wab_step_small<8, 0, false, true>(Params);
+template __global__ void wab_step_small<8, 0, true, true>(Params);
 template __global__ void wab_step_small<8, 11, false, false>(Params);
 template __global__ void wab_step_small<8, 11, true, false>(Params);
 template __global__ void wab_step_small<8, 11, false, true>(Params);
+template __global__ void wab_step_small<8, 11, true, true>(Params);
 template __global__ void wab_step_small<16, 0, false, false>(Params);
 template __global__ void wab_step_small<16, 0, true, false>(Params);
 template __global__ void wab_step_small<16, 0, false, true>(Params);
+template __global__ void wab_step_small<16, 0, true, true>(Params);
 template __global__ void wab_step_small<16, 11, false, false>(Params);
 template __global__ void wab_step_small<16, 11, true, false>(Params);
 template __global__ void wab_step_small<16, 11, false, true>(Params);
+template __global__ void wab_step_small<16, 11, true, true>(Params);
 template __global__ void wab_step_small<32, 0, false, false>(Params);
 template __global__ void wab_step_small<32, 0, true, false>(Params);
 template __global__ void wab_step_small<32, 0, false, true>(Params);
+template __global__ void wab_step_small<32, 0, true, true>(Params);
 template __global__ void wab_step_small<32, 11, false, false>(Params);
 template __global__ void wab_step_small<32, 11, true, false>(Params);
 template __global__ void wab_step_small<32, 11, false, true>(Params);
+template __global__ void wab_step_small<32, 11, true, true>(Params);
 
 }  // namespace wab

@@ -282,6 +282,55 @@ class BatchedWolvesAndBushesEnv:
                    "wab_rollout")
         return planes, scal.permute(1, 0, 2), rew, done
 
+    def rollout_features(self, actions, gamma=0.99, bootstrap=None, returns=True, store_planes=False,
+                         features=None):
+        """T steps of PragmaticObsWrapper(env).step with the actions [T, B] (the loop of
+        actor_critic.main, actor_critic.py:185-200) and finish_episode's discounted returns of
+        the segment (actor_critic.py:139-143; R after the last step = bootstrap [B] or 0), one
+        launch where the fused small-view kernel applies (wab_rollout_features).  Returns a dict:
+        features [T,B,F] f32, scalars [T,3,B], reward [T,B], done [T,B], returns [T,B] f32 (or
+        None), planes [T,B,3,W,S] (or None unless store_planes).  Bit for bit T step_features()
+        calls followed by discounted_returns(env=self)."""
+        t = self._torch
+        a = t.as_tensor(actions, device=self.device)
+        if a.dim() != 2 or a.shape[1] != self.num_envs:
+            raise ValueError("actions must have shape [T, num_envs]")
+        self._sync_action_check(a)
+        if a.dtype != t.int8:
+            a = a.clamp(-1, 127)
+        a = a.to(t.int8).contiguous()
+        T, B = a.shape
+        L = _lib.load()
+        F = int(L.wab_feature_dim(self._h))
+        if F < 0:
+            raise ValueError("PragmaticObsWrapper cannot index this viewport")
+        if features is None:
+            features = t.empty((T, B, F), dtype=t.float32, device=self.device)
+        elif (features.dtype != t.float32 or tuple(features.shape) != (T, B, F) or not features.is_contiguous()
+              or features.device != self.device):
+            raise ValueError("features must be a contiguous float32 tensor of shape (%d, %d, %d) on %s"
+                             % (T, B, F, self.device))
+        planes = (t.empty((T, B, 3, self.W, self.S), dtype=t.uint8, device=self.device) if store_planes
+                  else None)
+        scal = t.empty((3, T, B), dtype=t.uint8, device=self.device)
+        rew = t.empty((T, B), dtype=t.float32, device=self.device)
+        done = t.empty((T, B), dtype=t.uint8, device=self.device)
+        ret = t.empty((T, B), dtype=t.float32, device=self.device) if returns else None
+        bs = None
+        if bootstrap is not None:
+            bs = t.as_tensor(bootstrap, device=self.device).to(t.float32).contiguous()
+            if bs.shape != (B,):
+                raise ValueError("bootstrap must have shape [num_envs]")
+        o = _lib.WabObs(None if planes is None else planes.data_ptr(), scal[0].data_ptr(), scal[1].data_ptr(),
+                        scal[2].data_ptr())
+        _lib.check(L.wab_rollout_features(self._h, a.data_ptr(), T, ctypes.addressof(o), rew.data_ptr(),
+                                          done.data_ptr(), features.data_ptr(), float(gamma),
+                                          None if bs is None else bs.data_ptr(),
+                                          None if ret is None else ret.data_ptr(), self._stream()),
+                   "wab_rollout_features")
+        return {"features": features, "scalars": scal.permute(1, 0, 2), "reward": rew, "done": done,
+                "returns": ret, "planes": planes}
+
     def render(self, mode="rgb_array", scale=32, draw_health=True, out=None, obs=None):
         """render (wab_env.py:468-502) of every env's current observation (or of `obs`, a
         dict of planes [B,3,W,S] and scalars [3,B] u8 tensors) on device: u8 [B, W*scale,

@@ -68,6 +68,15 @@ class PragmaticObsWrapper:
         self.env.reset(mask)
         return self.observation()
 
+    def rollout(self, actions, gamma=0.99, bootstrap=None):
+        """T steps of this wrapper with the actions [T, B] and the discounted returns of the
+        segment (actor_critic.py:139-143, 185-200): (features [T,B,F], reward [T,B], done [T,B],
+        returns [T,B]), one kernel launch where the fused path applies (env.rollout_features)."""
+        if type(self) is not PragmaticObsWrapper:
+            raise NotImplementedError("rollout() fuses PragmaticObsWrapper only")
+        r = self.env.rollout_features(actions, gamma=gamma, bootstrap=bootstrap)
+        return r["features"], r["reward"], r["done"].view(self.env._torch.bool), r["returns"]
+
     def step(self, actions):
         if self.env._term is None and type(self) is PragmaticObsWrapper:
             # one kernel: the step and the features of its obs (wab_step_features)
