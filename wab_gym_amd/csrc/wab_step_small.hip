@@ -632,7 +632,7 @@ __device__ __forceinline__ void new_episode_b(const Params& p, const Lds& s, int
 // multi-step launches: the view-mask zero lines stored early in each step (1) or with the rest
 // of the rows (0) (A/B)
 #ifndef WAB_ROLL_EARLY_VIEWS
-#define WAB_ROLL_EARLY_VIEWS 1
+#define WAB_ROLL_EARLY_VIEWS 0
 #endif
 
 // --------------------------------------------------------------------------- fused features: early lines
@@ -1435,7 +1435,7 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
 // all 256 threads expand the feature bits to float32 (the featurizer's phases 2 and 3).
 // multi-step launches: feature rows non-temporal (1) or plain (0) (A/B)
 #ifndef WAB_ROLL_FEAT_NT
-#define WAB_ROLL_FEAT_NT 0
+#define WAB_ROLL_FEAT_NT 1
 #endif
 template <bool ROLL = false>
 __device__ __forceinline__ void step_features(const Params& p, const SmallLayout& L, uint32_t* lds, int wave,
