@@ -223,6 +223,10 @@ def main():
                          "instead of one launch per step; 0: per-step launches; default: %d for the "
                          "default config and c5 (the small kernel's multi-step build), 0 otherwise"
                          % DEFAULT_ROLLOUT)
+    ap.add_argument("--obs-ring", type=int, default=0,
+                    help="per-step launches: N > 0 writes step t's obs, reward and done into slot t %% N of "
+                         "[N, B] buffers (the stores then reach HBM, as a rollout's do) instead of one "
+                         "[B] buffer rewritten every step (which a 256 MB Infinity Cache can absorb)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
@@ -346,6 +350,23 @@ def main():
             for t in range(t0, t0 + n, T):
                 _lib.check(L.wab_rollout(h, a0 + t * B, T, seq_addr, seq_rew.data_ptr(), seq_done.data_ptr(), s),
                            "wab_rollout")
+    elif args.obs_ring > 0:
+        N = args.obs_ring
+        ring_planes = torch.empty((N, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+        ring_scal = torch.empty((3, N, B), dtype=torch.uint8, device=dev)
+        ring_rew = torch.empty((N, B), dtype=torch.float32, device=dev)
+        ring_done = torch.empty((N, B), dtype=torch.uint8, device=dev)
+        ring_slots = [_lib.WabObs(ring_planes[i].data_ptr(), ring_scal[0, i].data_ptr(), ring_scal[1, i].data_ptr(),
+                             ring_scal[2, i].data_ptr()) for i in range(N)]
+        slot_addr = [ctypes.addressof(o) for o in ring_slots]
+
+        def run(t0, n, stream):
+            s = ctypes.c_void_p(stream.cuda_stream)
+            for t in range(t0, t0 + n):
+                i = t % N
+                rc = L.wab_step(h, a0 + t * B, slot_addr[i], ring_rew[i].data_ptr(), ring_done[i].data_ptr(), None, s)
+                if rc:
+                    _lib.check(rc, "wab_step")
     else:
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
@@ -533,7 +554,9 @@ def main():
                                            if rollout else
                                            "; %d-step wab_rollout_features launches (features, reward, done, "
                                            "returns into [%d, B] rollout buffers)" % (T_roll, T_roll)
-                                           if c5_roll else "; one step launch per step"),
+                                           if c5_roll else
+                                           "; one step launch per step, obs into a %d-slot ring" % args.obs_ring
+                                           if args.obs_ring > 0 else "; one step launch per step"),
                        "batch_per_gpu": B, "global_batch": B * world,
                        "viewport": [Wv, Hv], "plane_stride": env.S, "wolf_slots": slots, "launch": args.mode,
                        "parallelism": "independent env shards x%d (no collective)" % world},

@@ -820,3 +820,69 @@ def test_rollout_features_full_size_c5():
             R = exact.get(np.float32(rt[t, b]), float(rt[t, b])) + 0.99 * R
             assert np.float32(R) == ret[t, b], (b, t)
     assert e1.counters() == e2.counters()
+
+
+# ------------------------------------------------------------------ the wide kernel's rollout build
+@pytest.mark.parametrize("opts,stride,slots,autoreset", [
+    ({"width": 31, "height": 31}, 32, 8, True),
+    ({"width": 31, "height": 31}, 32, 32, True),
+    ({"width": 31, "height": 31, "chance_wolf_on_square": 0.01, "wolf_chance_to_despawn": 0.2,
+      "wolf_spawn_margin": 2}, 32, 32, True),                          # HBM wolf rows every step
+    ({"width": 31, "height": 31, "chance_wolf_on_square": 0.01, "wolf_chance_to_despawn": 0.2,
+      "wolf_spawn_margin": 2}, 32, 16, True),                          # ... and the cap
+    ({"width": 17, "height": 13, "lookout_only": False}, 16, 8, True),
+    ({"width": 25, "height": 29, "starting_food": None, "starting_role": None}, 32, 16, True),
+    ({"width": 31, "height": 15, "wolves_can_move": False, "god_mode": True}, 16, 8, True),
+    ({"width": 13, "height": 11, "turns_to_fill_food": 4, "max_turns": 60, "bush_power": 60}, 16, 8, True),
+    ({"width": 31, "height": 31}, 32, 16, False),                     # stepping past done
+])
+def test_wide_rollout_equals_step_loop(opts, stride, slots, autoreset):
+    """wab_rollout on the wide kernel (one launch of T steps, state carried on chip) == T wab_step
+    calls, bit for bit, over two consecutive rollouts, a partial last group included; final hidden
+    state and counters equal too."""
+    import torch
+
+    B, T = 1000, 45
+    rs = np.random.RandomState(13)
+    kw = dict(validate_actions=False, plane_stride=stride, wolf_slots=slots, autoreset=autoreset)
+    e1, e2 = _env(opts, B, **kw), _env(opts, B, **kw)
+    assert e1.step_kernel == "wide"
+    e1.reset()
+    e2.reset()
+    for seg in range(2):
+        a = torch.as_tensor(rs.randint(e1.n_actions, size=(T, B)))
+        planes, scal, rew, done = e1.rollout(a)
+        for t in range(T):
+            obs, r, d, _ = e2.step(a[t])
+            assert torch.equal(planes[t], e2._obs["planes"]), (seg, t)
+            assert torch.equal(scal[t], e2._obs["scalars"]), (seg, t)
+            assert torch.equal(rew[t], r) and torch.equal(done[t].bool(), d), (seg, t)
+    s1, s2 = e1.state(), e2.state()
+    for k in s1:
+        assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
+    assert e1.counters() == e2.counters()
+
+
+def test_wide_rollout_full_size_c3():
+    """C3 at full size (B = 65536, 31x31 in 32x32 planes, 8 register wolves + HBM rows to 32):
+    two 32-step rollout launches == 64 wab_step launches, bit for bit, past the first mass reset."""
+    import torch
+
+    B, T = 65536, 32
+    kw = dict(validate_actions=False, plane_stride=32, wolf_slots=32)
+    opts = {"width": 31, "height": 31}
+    e1, e2 = _env(opts, B, **kw), _env(opts, B, **kw)
+    e1.reset()
+    e2.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(17)
+    for seg in range(2):
+        a = torch.randint(0, 5, (T, B), device="cuda:0", generator=g).to(torch.int8)
+        planes, scal, rew, done = e1.rollout(a)
+        for t in range(T):
+            e2.step(a[t])
+            assert torch.equal(planes[t], e2._obs["planes"]), (seg, t)
+            assert torch.equal(rew[t], e2.reward) and torch.equal(done[t].bool(), e2.done.bool()), (seg, t)
+            assert torch.equal(scal[t], e2._obs["scalars"]), (seg, t)
+        del planes
+    assert e1.counters() == e2.counters()

@@ -1,0 +1,7 @@
+# wide rollout build: parity, then C3 bench rollout vs per-step
+set -e
+o=gpurun_out/s2e
+mkdir -p $o
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "wide_rollout" -x -v --timeout 300 --timeout-method thread > $o/wide_roll_tests.log 2>&1
+timeout -k 10 300 python bench.py --config wide31 --rollout 32 --no-cpu > $o/bench_wide31_roll.log 2>&1
+timeout -k 10 300 python bench.py --config wide31 --rollout 0 --no-cpu > $o/bench_wide31_step.log 2>&1

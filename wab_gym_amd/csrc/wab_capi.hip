@@ -25,6 +25,8 @@ template <int SLOTS, int G, bool FEAT, bool ROLL>
 __global__ void wab_step_small(Params p);
 template <int MODE, int SLOTS>
 __global__ void wab_step_wide(Params p);
+template <int SLOTS>
+__global__ void wab_rollout_wide(Params p);
 
 __global__ void wab_featurize_kernel(FeatParams p);
 __global__ void wab_featurize_small_kernel(FeatParams p);
@@ -607,7 +609,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     }
     if (const char* kb = std::getenv("WAB_WIDE_LDS_KB"))
       h->wide_lds_bytes = std::max(h->wide_lds_bytes, (size_t)std::atoi(kb) * 1024u);
-    for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots)})
+    for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots),
+                    reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots>)})
       if (e == hipSuccess)
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_lds_bytes);
   }
@@ -689,7 +692,9 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
   if (int rc = check_obs(obs_seq, "wab_rollout")) return rc;
   const int64_t B = h->p.B;
   const size_t OB = (size_t)h->p.OB;
-  if (T > 0 && h->step_kernel == KERNEL_SMALL && h->reset_done && actions && reward && done &&
+  const char* wr = std::getenv("WAB_WIDE_ROLLOUT");  // A/B: 0 = T wab_step launches on the wide kernel
+  const bool wide_roll = h->step_kernel == KERNEL_WIDE && !(wr && std::atoi(wr) == 0);
+  if (T > 0 && (h->step_kernel == KERNEL_SMALL || wide_roll) && h->reset_done && actions && reward && done &&
       ((size_t)B * OB) % 16u == 0) {  // (every step's planes 16-byte aligned)
     // one launch: each workgroup runs its 64 envs through the T steps (Params::n_steps)
     Params p = h->p;
@@ -702,6 +707,13 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
     p.done = done;
     p.n_steps = T;
     DeviceGuard guard(h->device);
+    if (h->step_kernel == KERNEL_WIDE) {
+      if (h->n_blocks == 0) return WAB_OK;
+      hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_lds_bytes,
+                         (hipStream_t)stream, p);
+      HIP_TRY(hipGetLastError());
+      return WAB_OK;
+    }
     return launch<0>(h, p, (hipStream_t)stream);
   }
   for (int32_t t = 0; t < T; ++t) {

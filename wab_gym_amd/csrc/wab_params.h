@@ -214,8 +214,13 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
 // env-major with a 33-dword pitch so that lanes (= envs) touching the same row hit
 // different banks (dwords)
 constexpr uint32_t kWidePitch = 33;
+constexpr int kWideLdsLog = 16;  // multi-step launches: eaten-log entries W0 keeps on chip (0..3 in
+                                 // registers, 4..15 in LDS; later ones, rare, in HBM)
 struct WideLayout {
-  uint32_t bm, wp, spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey, total;
+  uint32_t bm, wp, spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey;
+  uint32_t nhdr, act, flag;  // multi-step launches: next headers (W0), next actions, W1 -> W0 flag
+  uint32_t elxy, elrem;      // multi-step launches: eaten-log entries 4..kWideLdsLog-1 (W0)
+  uint32_t total;
 };
 
 __host__ __device__ inline WideLayout wide_layout(const Params& p) {
@@ -235,6 +240,11 @@ __host__ __device__ inline WideLayout wide_layout(const Params& p) {
   L.blk = o; o += 4u;                         // n_jobs, job mask lo, hi
   L.jobEnv = o; o += 64u;
   L.jobKey = o; o += 128u;
+  L.nhdr = o; o += 64u * 4u;                  // uint4 per env
+  L.act = o; o += 16u;                        // 64 int8 actions
+  L.flag = o; o += 4u;
+  L.elxy = o; o += 64u * (uint32_t)(kWideLdsLog - 4);      // [entry - 4][env] tiles
+  L.elrem = o; o += 16u * (uint32_t)(kWideLdsLog - 4);     // [entry - 4][env] berries left (bytes)
   L.total = o;
   return L;
 }

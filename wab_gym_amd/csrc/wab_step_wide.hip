@@ -812,6 +812,649 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
 #endif
 }
 
+// --------------------------------------------------------------------------- multi-step launches
+// wab_rollout on the wide kernel: each workgroup takes its 64 envs through Params::n_steps steps
+// in one launch (the envs of a workgroup depend on nothing outside it).  The phases of a step
+// are those of wab_step_wide<MODE_STEP>; what changes is where the state lives between steps:
+//   - every wave: the env's header (W0 writes the next one to LDS, nhdr) and the next step's
+//     actions (W3 prefetches them with one scalar load per group into LDS, act);
+//   - W0: food, the 8 register wolf slots (uncompacted, with a live mask; the rarely used rows
+//     8.. stay in HBM, compacted at rows 8..8+nsp-1, read and written by the env's own lane) and
+//     the first four eaten-log entries (entries >= 4 in HBM, own lane);
+//   - W1: the view bitmap stays in LDS (bm), post-eat, new episodes' rows included.
+// Only step 0 loads state and only the last step stores it: after step 0 no wave issues a
+// vector load on its common path, so nothing waits for the previous steps' obs stores, and a
+// step's obs drain overlaps the next step's dynamics.  W0 (which owns the eaten log) clears the
+// emptied tiles that scrolled back into view from the bitmap after W1's scroll (LDS flag; the
+// per-step kernel has W1 do it from its own loads of the log).  Co-located wolves are
+// interchangeable (their despawn keys are (tile, occurrence index) whatever their order), so
+// the uncompacted slots step exactly as the per-step kernel's compacted rows do.
+namespace {
+
+// W1 -> W0 in step t: the scroll of step t is in bm (value t + 1: no clearing between steps)
+__device__ __forceinline__ void lds_publish_step(uint32_t* flag, uint32_t v) {
+  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_await_step(const Params& p, const uint32_t* flag, uint32_t v) {
+  for (int spin = 0; spin < (1 << 20); ++spin) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  atomicAdd(&p.counters[CTR_HANDOFF_TIMEOUTS], 1ull);
+}
+
+// whead of a carried header and action
+__device__ __forceinline__ WHead whead_of(const Params& p, int64_t g, bool active, uint4 hdr, int a) {
+  WHead h;
+  h.active = active;
+  h.hdr = active ? hdr : make_uint4(0u, 0u, 0u, 0u);
+  a = active ? a : 0;
+  h.kenv = env_key(p.seed, (uint64_t)(p.env_base + g));
+  h.ox = xy_x(h.hdr.x);
+  h.oy = xy_y(h.hdr.x);
+  h.turn = (int32_t)h.hdr.y + 1;
+  h.role = (int)misc_role(h.hdr.z);
+  h.dir = DIR_STAY;
+  h.valid_action = a >= 0 && a < p.n_actions;
+  if (h.valid_action) {
+    int dx, dy, nr;
+    decode_action(p, a, dx, dy, nr);
+    h.ox += dx;
+    h.oy += dy;
+    h.dir = dx > 0 ? DIR_RIGHT : dx < 0 ? DIR_LEFT : dy > 0 ? DIR_UP : dy < 0 ? DIR_DOWN : DIR_STAY;
+    if (nr >= 0) h.role = nr;
+  }
+  h.cpos = xy_pack(h.ox, h.oy);
+  const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
+  h.b0 = (uint32_t)ek;
+  h.b1 = (uint32_t)(ek >> 32);
+  return h;
+}
+
+// the next step's 64 actions of the group into act: one 64-byte scalar load (lgkmcnt: no wait
+// on this wave's stores), spread over lanes 0..15; a partial or misaligned group reads per lane
+__device__ __forceinline__ void wide_prefetch_actions(const Params& p, uint32_t* act, int lane) {
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const int8_t* a = p.actions + p.B + g0;  // step t + 1 (p.actions is step t's slice)
+  if (g0 + 64 <= p.B && (reinterpret_cast<uintptr_t>(a) & 3u) == 0u) {
+    typedef const uint32_t __attribute__((address_space(4))) CU32;
+    CU32* c = (CU32*)reinterpret_cast<uintptr_t>(a);
+    asm volatile("" : "+s"(c));
+    uint32_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = c[k];
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d = lane == k ? v[k] : d;
+    if (lane < 16) act[lane] = d;
+  } else {
+    const int8_t v = g0 + lane < p.B ? a[lane] : (int8_t)0;
+    reinterpret_cast<int8_t*>(act)[lane] = v;
+  }
+}
+
+// register slot k := v (k dynamic)
+template <int SLOTS>
+__device__ __forceinline__ void slot_set(uint32_t (&wr)[SLOTS], int k, uint32_t v) {
+#pragma unroll
+  for (int j = 0; j < SLOTS; ++j) wr[j] = j == k ? v : wr[j];
+}
+
+// step t of a multi-step launch: the I/O arrays advanced to their [t] slices
+__device__ __forceinline__ void wide_step_slice(Params& p, int t) {
+  const int64_t o = (int64_t)t * p.B;
+  p.actions += o;
+  p.planes += o * p.OB;
+  p.food_turns += o;
+  p.role += o;
+  p.status += o;
+  p.reward += o;
+  p.done += o;
+}
+
+}  // namespace
+
+template <int SLOTS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wab_rollout_wide(Params p0) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  if (g0 >= p0.B) return;  // (uniform over the workgroup)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int T = p0.n_steps;
+  const int n_active = (int)min((int64_t)64, p0.B - g0);
+  const int64_t g = g0 + lane;
+  const bool active = lane < n_active;
+  constexpr uint32_t P = kWidePitch;
+  const uint32_t me = (uint32_t)lane * P;
+
+  // carried state (per wave: the header; W0: food, wolves, eaten log)
+  uint4 hdr = make_uint4(0u, 0u, 0u, 0u);
+  double food = 0.0;
+  uint32_t wr[SLOTS];
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
+  uint32_t live = 0;  // occupied register slots
+  int nsp = 0;        // wolves in HBM rows SLOTS..SLOTS+nsp-1
+  uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
+  {  // the W1 -> W0 step flag starts below every step's value
+    const WideLayout L = wide_layout(p0);
+    if (tid == 0) lds[L.flag] = 0u;
+    lds_barrier();
+  }
+
+  for (int t = 0; t < T; ++t) {
+    const bool last = t == T - 1;
+    Params p = kernel_params(p0);
+    wide_step_slice(p, t);
+    const WideLayout L = wide_layout(p);
+    uint32_t* bm = lds + L.bm;
+    uint32_t* wp = lds + L.wp;
+    uint32_t* spawn = lds + L.spawn;
+    uint32_t* ring = lds + L.ring;
+    uint64_t* gap = reinterpret_cast<uint64_t*>(lds + L.gap);
+    uint64_t* thr = reinterpret_cast<uint64_t*>(lds + L.thr) + 1;
+    uint32_t* cval = lds + L.cval;
+    uint32_t* info = lds + L.info;
+    uint32_t* blk = lds + L.blk;
+    uint32_t* jobEnv = lds + L.jobEnv;
+    uint32_t* jobKey = lds + L.jobKey;
+    uint4* nhdr = reinterpret_cast<uint4*>(lds + L.nhdr);
+    uint32_t* act = lds + L.act;
+    uint32_t* flag = lds + L.flag;
+    uint32_t* elxy = lds + L.elxy;
+    uint8_t* elrem = reinterpret_cast<uint8_t*>(lds + L.elrem);
+    // eaten-log entry i >= 4 of this lane's env: LDS below kWideLdsLog, else HBM (rare; a load
+    // there waits for this wave's outstanding stores)
+    auto log_xy = [&](int i) -> uint32_t {
+      return i < kWideLdsLog ? elxy[(i - 4) * 64 + lane] : p.eaten_xy[(int64_t)i * p.B + g];
+    };
+    auto log_rem = [&](int i) -> uint32_t {
+      return i < kWideLdsLog ? (uint32_t)elrem[(i - 4) * 64 + lane] : (uint32_t)p.eaten_rem[(int64_t)i * p.B + g];
+    };
+    const uint32_t OB = (uint32_t)p.OB;
+    uint8_t* out = p.planes + (size_t)g0 * OB;
+    const int RW = (p.R + 31) >> 5;
+
+    int a = 0;
+    if (t == 0) {
+      if (active) {
+        hdr = p.hdr[g];
+        a = (int)p.actions[g];
+      }
+    } else {
+      hdr = nhdr[lane];
+      a = (int)reinterpret_cast<const int8_t*>(act)[lane];
+    }
+    const WHead h = whead_of(p, g, active, hdr, a);
+    int status = 0, ne = 0, ndep = 0;
+    bool job = false, emptied = false;
+    unsigned long long eaten_of = 0, wolf_of = 0;
+    uint32_t spill_live = 0;
+
+    if (wave == 0) {
+      // ------------------------------------------------ W0 P0: (loads,) despawn, pursuit, kill, wolf grid
+      __builtin_amdgcn_s_setprio(3);
+      const int nw0 = (int)misc_nw(h.hdr.z);
+      if (t == 0) {
+        if (active) {
+          food = p.food[g];
+#pragma unroll
+          for (int k = 0; k < SLOTS; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < p.eaten_cap) {
+              lxy[i] = p.eaten_xy[(int64_t)i * p.B + g];
+              lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
+            }
+          const int ne0 = (int)misc_ne(h.hdr.z);  // entries 4.. on chip (step 0: nothing stored yet)
+          for (int i = 4; i < ne0 && i < kWideLdsLog; ++i) {
+            elxy[(i - 4) * 64 + lane] = p.eaten_xy[(int64_t)i * p.B + g];
+            elrem[(i - 4) * 64 + lane] = p.eaten_rem[(int64_t)i * p.B + g];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k) opaque(wr[k]);
+        opaque(food);
+        live = nw0 >= 32 ? ~0u : ((1u << nw0) - 1u);
+        live &= (SLOTS >= 32 ? ~0u : ((1u << SLOTS) - 1u));
+        nsp = nw0 > SLOTS ? nw0 - SLOTS : 0;
+      }
+      if (!active) {
+        live = 0u;
+        nsp = 0;
+      }
+      for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;
+      ne = (int)misc_ne(h.hdr.z);
+      ndep = (int)misc_ndep(h.hdr.z);
+      const int status_old = (int)misc_status(h.hdr.z);
+      {  // despawn (:262-264), groups of 4 register slots; then the HBM rows
+        uint32_t keep = 0;
+#pragma unroll
+        for (int g4 = 0; g4 < SLOTS; g4 += 4) {
+          const uint32_t live4 = (live >> g4) & 0xFu;
+          if (!live4) continue;
+          uint32_t h1[4], hh[4], ts[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int k = g4 + q;
+            uint32_t occ = 0;
+#pragma unroll
+            for (int u = 0; u < k; ++u) occ += (((live >> u) & 1u) && wr[u] == wr[k]) ? 1u : 0u;
+            ts[q] = make_ts(SITE_DESPAWN, occ, h.turn);
+            h1[q] = wr[k] ^ h.b0;
+          }
+          fmix32x4(h1);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hh[q] = h1[q] ^ ts[q] ^ h.b1;
+          fmix32x4(hh);
+          uint32_t kp = 0, tie = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            kp |= (hh[q] > p.keep_th ? 1u : 0u) << q;
+            tie |= (hh[q] == p.keep_th ? 1u : 0u) << q;
+          }
+          if (tie & live4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (((tie >> q) & 1u) && draw_lo21(h1[q], ts[q], h.b0) >= p.keep_tl) kp |= 1u << q;
+          }
+          keep |= (kp & live4) << g4;
+        }
+        if (nsp > 0) spill_live = spill_despawn<SLOTS>(p, h, g, SLOTS + nsp, wr, live);
+        live = keep;
+      }
+      bool kill = false;
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) {  // pursuit (:267-286), grid of S (:412-428), kill (:291-297)
+        if (!((live >> k) & 1u)) continue;
+        int wx = xy_x(wr[k]), wy = xy_y(wr[k]);
+        if (p.wolves_can_move) {
+          const int ddx = h.ox - wx, ddy = h.oy - wy;
+          const bool alongx = abs(ddx) >= abs(ddy);
+          wx += alongx ? sgn(ddx) : 0;
+          wy += alongx ? 0 : sgn(ddy);
+          wr[k] = xy_pack(wx, wy);
+        }
+        const int ddx = h.ox - wx, ddy = h.oy - wy;
+        if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
+        kill |= ddx == 0 && ddy == 0;
+      }
+      if (spill_live) {  // the surviving HBM-row wolves: pursued in place
+        for (uint32_t bits = spill_live; bits; bits &= bits - 1u) {
+          const int k = SLOTS + __ffs(bits) - 1;
+          const uint32_t w = pursue(p, h, p.wolves[(int64_t)k * p.B + g]);
+          p.wolves[(int64_t)k * p.B + g] = w;
+          const int ddx = h.ox - xy_x(w), ddy = h.oy - xy_y(w);
+          if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) wp[me + (uint32_t)(ddx + p.cw)] |= 1u << (ddy + p.ch);
+          kill |= ddx == 0 && ddy == 0;
+        }
+      }
+      kill = kill && !p.god_mode;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      obs_plane<0>(p, wp, out, (uint32_t)n_active, lane);
+      // emptied tiles that scrolled back into view are absent from S (:506): cleared from the
+      // bitmap once W1 has scrolled it (the per-step kernel's W1 does this from its own loads)
+      const bool clear = active && ndep > 0 && h.dir != DIR_STAY;
+      if (__ballot(clear)) {
+        lds_await_step(p, flag, (uint32_t)t + 1u);
+        if (clear) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int ddx = h.ox - xy_x(lxy[k]), ddy = h.oy - xy_y(lxy[k]);
+            if (k < ne && lrem[k] == 0u && abs(ddx) <= p.cw && abs(ddy) <= p.ch)
+              bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+          }
+          for (int i = 4; i < ne; ++i) {  // (more than 4 eaten tiles this episode)
+            if (log_rem(i) != 0u) continue;
+            const uint32_t tt = log_xy(i);
+            const int ddx = h.ox - xy_x(tt), ddy = h.oy - xy_y(tt);
+            if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+          }
+        }
+      }
+      int found = -1, found_rem = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < ne && lxy[k] == h.cpos) { found = k; found_rem = (int)lrem[k]; }
+      lds_barrier();  // B1
+      // ------------------------------------------------ W0 P1: eat, starve, done; then obs
+      double reward = 0.0;
+      if (active) {
+        const bool center_bush = ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u) != 0u;
+        if (center_bush && found < 0 && ne > 4) {
+          for (int i = 4; i < ne; ++i)
+            if (log_xy(i) == h.cpos) { found = i; found_rem = (int)log_rem(i); }
+        }
+        const int rem = found >= 0 ? found_rem : (center_bush ? (int)cval[lane] : 0);
+        if (rem > 0 && status_old == 0 && (h.role == 1 || p.lookout_only)) {  // eat (:299-313)
+          food = food + p.fill;
+          food = food < 0.0 ? 0.0 : (food > 1.0 ? 1.0 : food);
+          reward += p.r_eat;
+          bool logged = true;
+          if (found >= 0 && found < 4) {  // (entries 0..3 live in registers)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (found == k) lrem[k] = (uint32_t)(rem - 1);
+          } else if (found >= 4) {  // (HBM written through: the state at the launch's end)
+            if (found < kWideLdsLog) elrem[(found - 4) * 64 + lane] = (uint8_t)(rem - 1);
+            p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
+          } else if (ne < p.eaten_cap) {
+            if (ne < 4) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                if (ne == k) {
+                  lxy[k] = h.cpos;
+                  lrem[k] = (uint32_t)(rem - 1);
+                }
+            } else {
+              if (ne < kWideLdsLog) {
+                elxy[(ne - 4) * 64 + lane] = h.cpos;
+                elrem[(ne - 4) * 64 + lane] = (uint8_t)(rem - 1);
+              }
+              p.eaten_xy[(int64_t)ne * p.B + g] = h.cpos;
+              p.eaten_rem[(int64_t)ne * p.B + g] = (uint8_t)(rem - 1);
+            }
+            ne += 1;
+          } else {
+            eaten_of += 1;
+            logged = false;
+          }
+          if (rem == 1) {
+            emptied = true;
+            if (logged) ndep += 1;
+          }
+        }
+        food = food - p.hunger;  // :316-322
+        const bool starved = food <= 0.0;
+        if (starved) food = 0.0;
+        status = starved ? 1 : kill ? 2 : status_old;
+        const bool done = starved || kill || status_old != 0 || h.turn >= p.max_turns;
+        {
+          const double r_finish = sreg(p.r_finish), r_turn = sreg(p.r_turn);
+          const double r_starve = sreg(p.r_starve), r_killed = sreg(p.r_killed);
+          reward += sel_f64(status == 0, sel_f64(done, r_finish, r_turn), sel_f64(status == 1, r_starve, r_killed));
+        }
+        job = done && p.autoreset;
+        __builtin_nontemporal_store((float)reward, p.reward + g);
+        __builtin_nontemporal_store((uint8_t)(done ? 1 : 0), p.done + g);
+        if (!job) {
+          p.food_turns[g] = (uint8_t)(int)ceil(food * (double)p.turns_empty);  // :450-452
+          p.role[g] = (uint8_t)h.role;
+          p.status[g] = (uint8_t)status;
+        }
+        if (!h.valid_action) atomicAdd(&p.counters[CTR_BAD_ACTIONS], 1ull);
+      }
+      info[lane] = (job ? 1u : 0u) | (emptied ? 2u : 0u);
+      const unsigned long long jm = __ballot(job);
+      if (job) {
+        const int j = __popcll(jm & ((1ull << lane) - 1ull));
+        const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
+        jobEnv[j] = (uint32_t)lane;
+        *reinterpret_cast<uint2*>(&jobKey[2 * j]) = make_uint2((uint32_t)ek2, (uint32_t)(ek2 >> 32));
+      }
+      if (lane == 0) {
+        blk[0] = (uint32_t)__popcll(jm);
+        blk[1] = (uint32_t)jm;
+        blk[2] = (uint32_t)(jm >> 32);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
+      lds_barrier();  // B2
+      // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
+      if (active && !job) {
+        int n_unplaced = 0;
+        if (p.wolves_on) {
+          for (int w = 0; w < RW; ++w) {
+            uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w];
+            while (bits) {
+              const int b = __ffs(bits) - 1;
+              bits &= bits - 1;
+              const uint32_t tt = xy_add(h.cpos, ring[32 * w + b]);
+              bool placed = false;
+#pragma unroll
+              for (int k = 0; k < SLOTS; ++k)
+                if (!placed && !((live >> k) & 1u)) { wr[k] = tt; live |= 1u << k; placed = true; }
+              n_unplaced += placed ? 0 : 1;
+            }
+          }
+        }
+        // the HBM rows: survivors compacted (row k read before any row >= its new index is
+        // written), then the spawns that found no register slot, up to the cap
+        int n = __popc(live);
+        int ns = 0;
+        for (uint32_t bits = spill_live; bits; bits &= bits - 1u) {
+          const int k = SLOTS + __ffs(bits) - 1;
+          if (k != SLOTS + ns) p.wolves[(int64_t)(SLOTS + ns) * p.B + g] = p.wolves[(int64_t)k * p.B + g];
+          ns += 1;
+        }
+        n += ns;
+        if (n_unplaced) {
+          int skip = -n_unplaced;
+          for (int w = 0; w < RW; ++w)
+            for (uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w]; bits; bits &= bits - 1u) skip += 1;
+          for (int w = 0; w < RW && n_unplaced; ++w) {
+            for (uint32_t bits = spawn[(uint32_t)lane * L.spw + (uint32_t)w]; bits; bits &= bits - 1u) {
+              if (skip > 0) { skip -= 1; continue; }
+              const uint32_t tt = xy_add(h.cpos, ring[32 * w + __ffs(bits) - 1]);
+              if (n < p.wolf_cap) {
+                p.wolves[(int64_t)(SLOTS + ns) * p.B + g] = tt;
+                ns += 1;
+                n += 1;
+              } else {
+                wolf_of += 1;
+              }
+            }
+          }
+        }
+        nsp = ns;
+        hdr = make_uint4(h.cpos, (uint32_t)h.turn,
+                         misc_pack((uint32_t)h.role, (uint32_t)status, (uint32_t)n, (uint32_t)ne, (uint32_t)ndep),
+                         h.hdr.w);
+        nhdr[lane] = hdr;
+        if (last) {  // the state, compacted as the per-step kernel leaves it
+          int m = 0;
+#pragma unroll
+          for (int k = 0; k < SLOTS; ++k)
+            if ((live >> k) & 1u) p.wolves[(int64_t)(m++) * p.B + g] = wr[k];
+          for (int i = 0; i < nsp; ++i)  // (m <= SLOTS: row SLOTS + i read before row m + i is written)
+            if (m < SLOTS) p.wolves[(int64_t)(m + i) * p.B + g] = p.wolves[(int64_t)(SLOTS + i) * p.B + g];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < ne && i < p.eaten_cap) {
+              p.eaten_xy[(int64_t)i * p.B + g] = lxy[i];
+              p.eaten_rem[(int64_t)i * p.B + g] = (uint8_t)lrem[i];
+            }
+          p.hdr[g] = hdr;
+          p.food[g] = food;
+        }
+      }
+    } else {
+      if (wave == 1) {
+        // ---------------------------------------------- W1 P0: the view bitmap
+        __builtin_amdgcn_s_setprio(2);
+        uint32_t w[32];
+        if (t == 0) {
+          const int nthr = p.max_berries;
+          uint64_t tv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
+          const int64_t ga = active ? g : 0;
+          const uint4* src = reinterpret_cast<const uint4*>(p.bushmap + (size_t)ga * 32u);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint4 v = src[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
+          if (lane == 0) bush_thr_pads(thr, nthr);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 32; ++i) w[i] = i < p.W ? bm[me + (uint32_t)i] : 0u;
+        }
+        const uint32_t strip = active ? strip_bits(p, h) : 0u;
+        const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
+        const uint32_t top = 1u << (p.H - 1);
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {  // scroll (:613-629) + the entering strip
+          if (i >= p.W) break;
+          const uint32_t wi = active ? w[i] : 0u;
+          const uint32_t prev = (active && i > 0) ? w[i - 1] : 0u;
+          const uint32_t next = (active && i < 31 && i + 1 < p.W) ? w[i + 1] : 0u;
+          const uint32_t sb = (strip >> i) & 1u;
+          uint32_t v = wi;
+          v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
+          v = h.dir == DIR_LEFT ? (i == p.W - 1 ? strip : next) : v;
+          v = h.dir == DIR_UP ? (((wi << 1) & hmask) | sb) : v;
+          v = h.dir == DIR_DOWN ? ((wi >> 1) | (sb ? top : 0u)) : v;
+          bm[me + (uint32_t)i] = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) lds_publish_step(flag, (uint32_t)t + 1u);  // (W0 clears the emptied tiles)
+        uint32_t cv = 0;  // the generated berries of the ostrich's tile (:631-635), for W0 (unused
+                          // when W0 clears that tile: it is then in the log with no berries)
+        if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
+          cv = (uint32_t)bush_value_fast(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1),
+                                         p.bush_power);
+        cval[lane] = cv;
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+        // ---------------------------------------------- W3: ostrich grids; W2: tables, spawn set
+        if (wave == 3) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
+        if (wave == 2) {
+          if (t == 0) {
+            copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
+            if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          }
+          for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          if (p.wolves_on && active)
+            spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
+              spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
+            });
+          obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
+        }
+      }
+      lds_barrier();  // B1
+      if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
+      if (wave < 3) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
+      lds_barrier();  // B2
+    }
+
+    const int n_jobs = (int)blk[0];
+    const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+    // ------------------------------------------------ P2: the continuing envs' bitmaps (post-eat)
+    if (tid < n_active && !((jmask >> tid) & 1ull) && (info[tid] & 2u))
+      bm[(uint32_t)tid * P + (uint32_t)p.cw] &= ~(1u << p.ch);  // eaten empty
+    if (wave == 0) {
+      if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
+      if (lane == 0 && n_jobs) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);
+      count_steps(p);
+    }
+    if (n_jobs > 0) {
+      // ------------------------------------------------ done envs: new episodes (:231-248)
+      lds_barrier();  // B3: the eaten-empty clears are in (a job's rows are redrawn below)
+      const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
+      const uint32_t rows2 = ((uint32_t)p.W + 1u) >> 1;
+      for (int jj = 0; jj < n_jobs; ++jj) {
+        const uint32_t e = jobEnv[jj];
+        const uint2 kq = *reinterpret_cast<const uint2*>(&jobKey[2 * jj]);
+        for (uint32_t r2 = (uint32_t)wave; r2 < rows2; r2 += 4u) {
+          const uint32_t i = 2u * r2 + ((uint32_t)lane >> 5), j = (uint32_t)lane & 31u;
+          const bool cell = i < (uint32_t)p.W && j < (uint32_t)p.H;
+          const uint32_t xy = xy_pack(p.cw - (int)i, p.ch - (int)j);
+          const uint32_t h1 = fmix32(xy ^ kq.x);
+          const uint32_t hb = fmix32(h1 ^ ts_bush ^ kq.y);
+          const bool bush = cell && U_ge(h1, hb, ts_bush, kq.x, p.bush_th, p.bush_tl);
+          const unsigned long long bb = __ballot(bush);
+          if ((lane & 31) == 0 && i < (uint32_t)p.W) bm[e * P + i] = (uint32_t)(lane ? bb >> 32 : bb);
+        }
+      }
+      if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
+        const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
+        for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;
+        if (p.wolves_on)
+          spawn_hits(gap, p.WH, p.gap_full_th, p.gap_full_tl, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, (uint32_t)ek2,
+                     (uint32_t)(ek2 >> 32), [&](int c) {
+                       const uint32_t i = (uint32_t)c / (uint32_t)p.H;
+                       wp[me + i] |= 1u << ((uint32_t)c - i * (uint32_t)p.H);
+                     });
+      }
+      lds_barrier();  // B4
+      if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
+        // spawn_ostriches (:595-611) and the initial wolves, one per wolf cell of the view
+        const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
+        const uint32_t kb0 = (uint32_t)ek2, kb1 = (uint32_t)(ek2 >> 32);
+        const double food2 = p.start_food_random
+                                 ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
+                                 : p.start_food;
+        const int role2 = p.start_role_random
+                              ? (int)(draw_U(xy_pack(0, 0), make_ts(SITE_START_ROLE, 0, 0), kb0, kb1) >> 52)
+                              : p.start_role;
+        int n = 0;
+        live = 0u;
+        for (int i = 0; i < p.W; ++i) {
+          uint32_t bits = wp[me + (uint32_t)i];
+          while (bits) {
+            const int j = __ffs(bits) - 1;
+            bits &= bits - 1;
+            const uint32_t tt = xy_pack(p.cw - i, p.ch - j);
+            if (n < SLOTS) {
+              slot_set<SLOTS>(wr, n, tt);
+              live |= 1u << n;
+              if (last) p.wolves[(int64_t)n * p.B + g] = tt;
+              n += 1;
+            } else if (n < p.wolf_cap) {
+              p.wolves[(int64_t)n * p.B + g] = tt;
+              n += 1;
+            } else {
+              wolf_of += 1;
+              atomicAdd(&p.counters[CTR_WOLF_OVERFLOW_RESET], 1ull);
+            }
+          }
+        }
+        nsp = n > SLOTS ? n - SLOTS : 0;
+        food = food2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          lxy[i] = 0u;
+          lrem[i] = 0u;
+        }
+        hdr = make_uint4(xy_pack(0, 0), 0u, misc_pack((uint32_t)role2, 0u, (uint32_t)n, 0u, 0u), h.hdr.w + 1u);
+        nhdr[lane] = hdr;
+        p.food_turns[g] = (uint8_t)(int)ceil(food2 * (double)p.turns_empty);
+        p.role[g] = (uint8_t)role2;
+        p.status[g] = 0;
+        if (last) {
+          p.hdr[g] = hdr;
+          p.food[g] = food2;
+        }
+      }
+      for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
+    }
+    if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
+    if (last) {  // every env's bitmap rows (continuing: post-eat; done: the new episode's)
+      lds_barrier();
+      for (uint32_t u = tid; u < 64u * 32u; u += 256) {
+        const uint32_t e = u >> 5, i = u & 31u;
+        if ((int)e >= n_active || i >= (uint32_t)p.W) continue;
+        p.bushmap[(size_t)(g0 + e) * 32u + i] = bm[e * P + i];
+      }
+    }
+    lds_barrier();  // the step's end: its LDS (bm, wp, nhdr, act) is the next step's input
+  }
+}
+
+template __global__ void wab_rollout_wide<8>(Params);
+
 #define WAB_WIDE_INST(M, S) template __global__ void wab_step_wide<M, S>(Params);
 WAB_WIDE_INST(MODE_STEP, 8)
 WAB_WIDE_INST(MODE_RESET, 8)
