@@ -220,9 +220,8 @@ def main():
     ap.add_argument("--rollout", type=int, default=-1,
                     help="T > 0: wab_rollout (c5: wab_rollout_features) segments of T steps (one "
                          "launch each; obs or features, reward, done into a [T, B] rollout buffer) "
-                         "instead of one launch per step; 0: per-step launches; default: %d for the "
-                         "default config and c5 (the small kernel's multi-step build), 0 otherwise"
-                         % DEFAULT_ROLLOUT)
+                         "instead of one launch per step; 0: per-step launches; default: %d (the "
+                         "small and wide kernels' multi-step builds)" % DEFAULT_ROLLOUT)
     ap.add_argument("--obs-ring", type=int, default=0,
                     help="per-step launches: N > 0 writes step t's obs, reward and done into slot t %% N of "
                          "[N, B] buffers (the stores then reach HBM, as a rollout's do) instead of one "
@@ -267,7 +266,7 @@ def main():
     slots = args.wolf_slots or slots
     c5 = args.config == "c5"
     if args.rollout < 0:
-        args.rollout = DEFAULT_ROLLOUT if args.config in ("default", "c5") and not args.c5_unfused else 0
+        args.rollout = DEFAULT_ROLLOUT if not args.c5_unfused else 0
     c5_roll = c5 and args.rollout > 0
     if c5_roll:
         args.rollout = C5_SEGMENT if args.rollout <= 0 else args.rollout

@@ -900,6 +900,33 @@ __device__ __forceinline__ void slot_set(uint32_t (&wr)[SLOTS], int k, uint32_t 
   for (int j = 0; j < SLOTS; ++j) wr[j] = j == k ? v : wr[j];
 }
 
+// WAB_WIDE_ROLL_LINES (multi-step launches): 1 = each step's obs as whole 128-byte lines, the
+// group's chunk in address order by all 256 threads after B2 (lines that touch a done env after
+// its new episode, B4); 0 = plane by plane as soon as each plane is final (the per-step kernel's
+// order: a line at a plane or env boundary is then written in two parts, microseconds apart)
+#ifndef WAB_WIDE_ROLL_LINES
+#define WAB_WIDE_ROLL_LINES 1
+#endif
+
+// the group's obs chunks (16 bytes) whose 128-byte line touches a done env (jm) iff `touching`,
+// from bm / wp (the step's snapshot S, or a done env's new episode) and the fixed ostrich grid
+__device__ __forceinline__ void obs_lines(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                          uint32_t n_active, unsigned long long jm, bool touching, int tid) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4;  // chunks per env (the group's chunk starts line-aligned:
+                                             // 64 * OB and B * OB are multiples of 128)
+  const uint32_t n = n_active * CPE;
+  uint32_t e = 0, r = (uint32_t)tid;
+  while (r >= CPE) { r -= CPE; ++e; }
+  for (uint32_t c = (uint32_t)tid; c < n; c += 256u) {
+    const uint32_t c0 = c & ~7u, c1 = min(c0 + 7u, n - 1u);  // the line's chunks
+    const uint32_t e0 = __umulhi(c0, p.magic_CPE), e1 = __umulhi(c1, p.magic_CPE);  // (c < 2^16: exact)
+    const bool t = ((jm >> e0) | (jm >> e1)) & 1ull;
+    if (t == touching) store16(p, out, c, expand16(chunk_bits(p, bm, wp, e, r)));
+    r += 256u;
+    while (r >= CPE) { r -= CPE; ++e; }
+  }
+}
+
 // step t of a multi-step launch: the I/O arrays advanced to their [t] slices
 __device__ __forceinline__ void wide_step_slice(Params& p, int t) {
   const int64_t o = (int64_t)t * p.B;
@@ -1090,9 +1117,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         }
       }
       kill = kill && !p.god_mode;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      obs_plane<0>(p, wp, out, (uint32_t)n_active, lane);
+      if (!WAB_WIDE_ROLL_LINES) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        obs_plane<0>(p, wp, out, (uint32_t)n_active, lane);
+      }
       // emptied tiles that scrolled back into view are absent from S (:506): cleared from the
       // bitmap once W1 has scrolled it (the per-step kernel's W1 does this from its own loads)
       const bool clear = active && ndep > 0 && h.dir != DIR_STAY;
@@ -1199,8 +1228,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         blk[2] = (uint32_t)(jm >> 32);
       }
       __builtin_amdgcn_s_setprio(0);
-      obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
+      if (!WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
+      if (WAB_WIDE_ROLL_LINES)  // S of the lines without a done env (the rest after B4)
+        obs_lines(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+                  false, tid);
       // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
       if (active && !job) {
         int n_unplaced = 0;
@@ -1296,6 +1328,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         } else {
 #pragma unroll
           for (int i = 0; i < 32; ++i) w[i] = i < p.W ? bm[me + (uint32_t)i] : 0u;
+          if (WAB_WIDE_ROLL_LINES) {  // the last step's eaten-empty tile (its S obs are stored)
+            const unsigned long long jmp = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+            if (lane < n_active && !((jmp >> lane) & 1ull) && (info[lane] & 2u)) {
+#pragma unroll
+              for (int i = 0; i < 32; ++i)
+                if (i == p.cw) w[i] &= ~(1u << p.ch);
+            }
+          }
         }
         const uint32_t strip = active ? strip_bits(p, h) : 0u;
         const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
@@ -1326,7 +1366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         __builtin_amdgcn_s_setprio(0);
       } else {
         // ---------------------------------------------- W3: ostrich grids; W2: tables, spawn set
-        if (wave == 3) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
+        if (wave == 3 && !WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
         if (wave == 2) {
           if (t == 0) {
             copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
@@ -1340,20 +1380,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
               spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
             });
-          obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
+          if (!WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
         }
       }
       lds_barrier();  // B1
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
-      if (wave < 3) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
+      if (wave < 3 && !WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
+      if (WAB_WIDE_ROLL_LINES)
+        obs_lines(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+                  false, tid);
     }
 
     const int n_jobs = (int)blk[0];
     const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
     // ------------------------------------------------ P2: the continuing envs' bitmaps (post-eat)
-    if (tid < n_active && !((jmask >> tid) & 1ull) && (info[tid] & 2u))
-      bm[(uint32_t)tid * P + (uint32_t)p.cw] &= ~(1u << p.ch);  // eaten empty
+    if (!WAB_WIDE_ROLL_LINES && tid < n_active && !((jmask >> tid) & 1ull) && (info[tid] & 2u))
+      bm[(uint32_t)tid * P + (uint32_t)p.cw] &= ~(1u << p.ch);  // eaten empty (LINES: by W1, next step)
     if (wave == 0) {
       if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
       if (lane == 0 && n_jobs) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);
@@ -1438,7 +1481,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food2;
         }
       }
-      for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
+      if (WAB_WIDE_ROLL_LINES)  // the lines that touch a done env: its new episode, its neighbours' S
+        obs_lines(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
+      else
+        for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
     }
     if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     if (last) {  // every env's bitmap rows (continuing: post-eat; done: the new episode's)
@@ -1446,7 +1492,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       for (uint32_t u = tid; u < 64u * 32u; u += 256) {
         const uint32_t e = u >> 5, i = u & 31u;
         if ((int)e >= n_active || i >= (uint32_t)p.W) continue;
-        p.bushmap[(size_t)(g0 + e) * 32u + i] = bm[e * P + i];
+        uint32_t v = bm[e * P + i];
+        if (WAB_WIDE_ROLL_LINES && !((jmask >> e) & 1ull) && (info[e] & 2u) && i == (uint32_t)p.cw) v &= ~(1u << p.ch);
+        p.bushmap[(size_t)(g0 + e) * 32u + i] = v;
       }
     }
     lds_barrier();  // the step's end: its LDS (bm, wp, nhdr, act) is the next step's input
