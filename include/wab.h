@@ -173,10 +173,13 @@ int wab_reset(wab_handle* h, const uint8_t* mask, const wab_obs* obs, void* stre
 int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward,
              uint8_t* done, const wab_obs* terminal, void* stream);
 
-/* T steps, stream-ordered (T step-kernel launches, no host synchronisation).
- * actions [T][B] int8; obs planes [T][B][3][width][plane_stride] and the scalar
- * arrays [T][B] (an obs "sequence"); reward/done [T][B].  Equivalent to T calls of
- * wab_step with terminal = NULL. */
+/* T steps, stream-ordered, no host synchronisation.  actions [T][B] int8; obs planes
+ * [T][B][3][width][plane_stride] and the scalar arrays [T][B] (an obs "sequence");
+ * reward/done [T][B].  Bit for bit T calls of wab_step with terminal = NULL.  Where the small
+ * or the wide kernel steps the handle (wab_step_kernel "small" / "wide") and B * width *
+ * plane_stride * 3 is a multiple of 16, this is ONE launch: each workgroup takes its 64 envs
+ * through the T steps with their state on chip (loaded by the first step, stored by the
+ * last); otherwise T wab_step launches. */
 int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq,
                 float* reward, uint8_t* done, void* stream);
 

@@ -325,8 +325,8 @@ __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u
     if (!(ROLL) || WAB_ROLL_PRIO != 0) __builtin_amdgcn_s_setprio(V); \
   } while (0)
 
-#ifndef WAB_W1_RESET_PRIO
-#define WAB_W1_RESET_PRIO 0
+#ifndef WAB_W1_RESET_PRIO  // multi-step launches only (per-step: 9.16-9.19 vs 9.13 us at 2)
+#define WAB_W1_RESET_PRIO 2
 #endif
 // the entering strip's cells are drawn in two parts, [0, kStripW1) on W1 after the tile value
 // and the rest on W3 after the spawn set (A/B: -DWAB_STRIP_W1=k)
@@ -1020,9 +1020,9 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   // flag[1] before it builds the new episodes
   const unsigned long long jm = __ballot(job);
   if (jm) {
-    // (W3 waits for these draws before it builds the new episodes: A/B of W1's issue priority
-    // while it makes them, WAB_W1_RESET_PRIO; 0 = unchanged)
-    if (WAB_W1_RESET_PRIO) WAB_PRIO(ROLL, WAB_W1_RESET_PRIO);
+    // (W3 waits for these draws before it builds the new episodes: W1 at issue priority 2
+    // while it makes them, multi-step launches: 6.41 -> 6.33 us per step, profiles/r03_ab2/)
+    if (ROLL && WAB_W1_RESET_PRIO) __builtin_amdgcn_s_setprio(WAB_W1_RESET_PRIO);
     if (job) {
       const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
       const int j = __popcll(jm & ((1ull << lane) - 1ull));
@@ -1030,7 +1030,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     }
     reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm);
     lds_publish(&s.flag[1]);
-    if (WAB_W1_RESET_PRIO) WAB_PRIO(ROLL, 0);
+    if (ROLL && WAB_W1_RESET_PRIO) __builtin_amdgcn_s_setprio(0);
   }
   if (early_obs(p)) {  // S was rendered by W2
     lds_await(p, &s.flag[2]);

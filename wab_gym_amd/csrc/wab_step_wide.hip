@@ -903,14 +903,14 @@ __device__ __forceinline__ void slot_set(uint32_t (&wr)[SLOTS], int k, uint32_t 
 // WAB_WIDE_ROLL_LINES (multi-step launches): 1 = each step's obs as whole 128-byte lines, the
 // group's chunk in address order by all 256 threads after B2 (lines that touch a done env after
 // its new episode, B4); 0 = plane by plane as soon as each plane is final (the per-step kernel's
-// order: a line at a plane or env boundary is then written in two parts, microseconds apart)
+// order: a line at a plane or env boundary is then written in two parts, microseconds apart).
+// Every store instruction must cover whole lines: a fixed chunk per thread over the envs (each
+// instruction 1 KiB contiguous, but an env-boundary line split between two instructions)
+// measured 49.9 us against 43.1 (profiles/r03_wideroll/ab_fixed/).
 #ifndef WAB_WIDE_ROLL_LINES
 #define WAB_WIDE_ROLL_LINES 1
 #endif
-// 1: obs_lines_fixed (a fixed chunk per thread), 0: obs_lines (A/B)
-#ifndef WAB_WIDE_LINES_FIXED
-#define WAB_WIDE_LINES_FIXED 1
-#endif
+
 
 // the group's obs chunks (16 bytes) whose 128-byte line touches a done env (jm) iff `touching`,
 // from bm / wp (the step's snapshot S, or a done env's new episode) and the fixed ostrich grid
@@ -928,35 +928,6 @@ __device__ __forceinline__ void obs_lines(const Params& p, const uint32_t* bm, c
     if (t == touching) store16(p, out, c, expand16(chunk_bits(p, bm, wp, e, r)));
     r += 256u;
     while (r >= CPE) { r -= CPE; ++e; }
-  }
-}
-
-// obs_lines with a fixed chunk per thread: thread r < CPE stores chunk r of every env of the
-// group (env e's chunk at e * CPE + r: each wave-instruction still 1 KiB contiguous), so its
-// plane, row and half, and the ostrich plane's bits, are computed once per step, not per chunk
-__device__ __forceinline__ void obs_lines_fixed(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
-                                                uint32_t n_active, unsigned long long jm, bool touching, int tid) {
-  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, WC = (uint32_t)p.W * CPR;
-  const uint32_t r = (uint32_t)tid;
-  if (r >= CPE) return;
-  const uint32_t k = (r >= WC ? 1u : 0u) + (r >= 2u * WC ? 1u : 0u);
-  const uint32_t r2 = r - k * WC;
-  const uint32_t i = CPR == 2u ? r2 >> 1 : r2, sh = CPR == 2u ? 16u * (r2 & 1u) : 0u;
-  const uint32_t* rows = (k == 0u ? wp : bm) + i;
-  const u32x4 ost = expand16(((i == (uint32_t)p.cw ? 1u << p.ch : 0u) >> sh) & 0xFFFFu);  // plane 2
-  const uint32_t n = n_active * CPE;
-  // the line of chunk e * CPE + r starts in env e - 1 iff its first chunk precedes the env's,
-  // ends in env e + 1 iff its last chunk passes the env's last (both fixed by r's offset mod 8
-  // and the env's start offset mod 8, which steps by CPE mod 8)
-  uint32_t c = r;
-  for (uint32_t e = 0; e < n_active; ++e, c += CPE) {
-    const uint32_t c0 = c & ~7u, c1 = c0 + 7u;
-    const uint32_t s0 = e * CPE;
-    const bool prev = c0 < s0, next = c1 >= s0 + CPE && c1 < n;
-    const bool tj = ((jm >> e) & 1ull) || (prev && ((jm >> (e - 1u)) & 1ull)) || (next && ((jm >> (e + 1u)) & 1ull));
-    if (tj != touching) continue;
-    const u32x4 v = k == 2u ? ost : expand16((rows[e * kWidePitch] >> sh) & 0xFFFFu);
-    store16(p, out, c, v);
   }
 }
 
@@ -1264,7 +1235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       if (!WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
       if (WAB_WIDE_ROLL_LINES)  // S of the lines without a done env (the rest after B4)
-        (WAB_WIDE_LINES_FIXED ? obs_lines_fixed : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+        obs_lines(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
       // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
       if (active && !job) {
@@ -1421,7 +1392,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       if (wave < 3 && !WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
       if (WAB_WIDE_ROLL_LINES)
-        (WAB_WIDE_LINES_FIXED ? obs_lines_fixed : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+        obs_lines(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
     }
 
@@ -1515,7 +1486,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         }
       }
       if (WAB_WIDE_ROLL_LINES)  // the lines that touch a done env: its new episode, its neighbours' S
-        (WAB_WIDE_LINES_FIXED ? obs_lines_fixed : obs_lines)(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
+        obs_lines(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
       else
         for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
     }
