@@ -432,6 +432,11 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
   }
 }
 
+// multi-step launches: the previous step's obs stored by W0, W2 and W3 (1; 8 units per thread)
+// or by W0 and W2 (0; 12 units per thread) in their slack before B2 (A/B)
+#ifndef WAB_ROLL_STORE_W3
+#define WAB_ROLL_STORE_W3 0
+#endif
 // multi-step launches: obs stores non-temporal (1) or plain (0) (A/B)
 #ifndef WAB_ROLL_NT
 #define WAB_ROLL_NT 1
@@ -899,7 +904,10 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     lds_await(p, &s.flag[2]);  // S rendered (W2)
     store_units(p, s.stream, jm, false, 0, 3, lane);
   }
-  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
+  if (ROLL && carry->prev_stream) {
+    if (WAB_ROLL_STORE_W3) store_units_nt<192, 8>(p, carry->prev_planes, carry->prev_stream, lane);
+    else store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
+  }
   SMALL_STAMP(4);
   lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
   if (p.t_planes) {
@@ -1214,7 +1222,10 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
   const unsigned long long jm = __ballot(job);
   if (early) store_units(p, s.stream, jm, false, 2, 3, lane);
-  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
+  if (ROLL && carry->prev_stream) {
+    if (WAB_ROLL_STORE_W3) store_units_nt<192, 8>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
+    else store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
+  }
   SMALL_STAMP(19);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -1250,7 +1261,8 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
 // --------------------------------------------------------------------------- W3: ring
 template <int SLOTS, int G, bool ROLL = false>
 __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane,
-                                                        CarryHdr* carry = nullptr, int t = 0, bool last = true) {
+                                                        CarryHdr* carry = nullptr, int t = 0, bool last = true,
+                                                        uint8_t* prev_planes = nullptr, uint32_t* prev_stream = nullptr) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
@@ -1339,6 +1351,8 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
       if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     }
   }
+  if (ROLL && WAB_ROLL_STORE_W3 && prev_stream)  // the third share of the last step's obs
+    store_units_nt<192, 8>(p, prev_planes, prev_stream, 128 + lane);
   SMALL_STAMP(25);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -1617,7 +1631,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
       WAB_ROLL_STEP((wolves_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1)))
     } else {
       CarryPtr<CarryHdr> c;
-      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1)))
+      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1, c.prev_planes, c.prev_stream)))
     }
 #undef WAB_ROLL_STEP
   }

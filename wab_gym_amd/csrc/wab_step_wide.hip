@@ -931,6 +931,75 @@ __device__ __forceinline__ void obs_lines(const Params& p, const uint32_t* bm, c
   }
 }
 
+// obs_lines by rows: thread q of the group's 3 W rows per env stores its row's CPR chunks with
+// consecutive instructions (one row read, one plane / row decode per row instead of per chunk);
+// for CPR = 2 an instruction covers every other 16 bytes and the next one the rest, so each
+// line is whole within two back-to-back instructions of one wave (merged in L2).  Envs that are
+// neither done nor next to a done env skip the line test.
+__device__ __forceinline__ void obs_rows(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                         uint32_t n_active, unsigned long long jm, bool touching, int tid) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W;
+  const uint32_t RPE = 3u * W;  // rows per env
+  const uint32_t n = n_active * CPE, nr = n_active * RPE;
+  const unsigned long long jn = jm | (jm << 1) | (jm >> 1);  // done envs and their neighbours
+  const uint32_t ost = 1u << p.ch;  // the ostrich grid's row cw
+  uint32_t e = 0, rr = (uint32_t)tid;
+  while (rr >= RPE) { rr -= RPE; ++e; }
+  for (uint32_t q = (uint32_t)tid; q < nr; q += 256u) {
+    const uint32_t k = (rr >= W ? 1u : 0u) + (rr >= 2u * W ? 1u : 0u);
+    const uint32_t i = rr - k * W;
+    const uint32_t c = e * CPE + rr * CPR;  // the row's first chunk
+    bool t = false;
+    if ((jn >> e) & 1ull) {
+      const uint32_t c0 = c & ~7u, c1 = min(c0 + 7u, n - 1u);
+      t = ((jm >> __umulhi(c0, p.magic_CPE)) | (jm >> __umulhi(c1, p.magic_CPE))) & 1ull;
+    }
+    if (t == touching) {
+      const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? ost : 0u) : (k == 0u ? wp : bm)[e * kWidePitch + i];
+      store16(p, out, c, expand16(v & 0xFFFFu));
+      if (CPR == 2u) store16(p, out, c + 1u, expand16(v >> 16));
+    }
+    rr += 256u;
+    while (rr >= RPE) { rr -= RPE; ++e; }
+  }
+}
+
+// S as soon as it is complete (B1) by the threads of W1..W3, every row whatever the env's fate;
+// after B4 the same threads (same mapping: program order per address) rewrite the rows of the
+// done envs with their new episode (those few lines are then written twice, the rest whole once)
+__device__ __forceinline__ void obs_rows_b1(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                            uint32_t n_active, unsigned long long jm, bool jobs_only, int idx) {
+  constexpr uint32_t NT = 192;
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W;
+  const uint32_t RPE = 3u * W;
+  const uint32_t nr = n_active * RPE;
+  const uint32_t ost = 1u << p.ch;
+  uint32_t e = 0, rr = (uint32_t)idx;
+  while (rr >= RPE) { rr -= RPE; ++e; }
+  for (uint32_t q = (uint32_t)idx; q < nr; q += NT) {
+    if (!jobs_only || ((jm >> e) & 1ull)) {
+      const uint32_t k = (rr >= W ? 1u : 0u) + (rr >= 2u * W ? 1u : 0u);
+      const uint32_t i = rr - k * W;
+      const uint32_t c = e * CPE + rr * CPR;
+      const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? ost : 0u) : (k == 0u ? wp : bm)[e * kWidePitch + i];
+      store16(p, out, c, expand16(v & 0xFFFFu));
+      if (CPR == 2u) store16(p, out, c + 1u, expand16(v >> 16));
+    }
+    rr += NT;
+    while (rr >= RPE) { rr -= RPE; ++e; }
+  }
+}
+#ifndef WAB_WIDE_S_AFTER_B1  // 1: obs_rows_b1 after B1 and for the done envs after B4 (A/B)
+#define WAB_WIDE_S_AFTER_B1 0
+#endif
+
+#ifndef WAB_WIDE_ROW_STORES  // 1: obs_rows, 0: obs_lines (A/B)
+#define WAB_WIDE_ROW_STORES 1
+#endif
+#ifndef WAB_WIDE_ROLL_FLOOR  // diagnostic: every step's work skipped, its obs stores kept
+#define WAB_WIDE_ROLL_FLOOR 0
+#endif
+
 // step t of a multi-step launch: the I/O arrays advanced to their [t] slices
 __device__ __forceinline__ void wide_step_slice(Params& p, int t) {
   const int64_t o = (int64_t)t * p.B;
@@ -1017,6 +1086,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       a = (int)reinterpret_cast<const int8_t*>(act)[lane];
     }
     const WHead h = whead_of(p, g, active, hdr, a);
+    if (WAB_WIDE_ROLL_FLOOR) {  // (A/B floor: the stores alone; results wrong by design)
+      lds_barrier();
+      (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid);
+      lds_barrier();
+      continue;
+    }
     int status = 0, ne = 0, ndep = 0;
     bool job = false, emptied = false;
     unsigned long long eaten_of = 0, wolf_of = 0;
@@ -1234,8 +1309,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       __builtin_amdgcn_s_setprio(0);
       if (!WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
-      if (WAB_WIDE_ROLL_LINES)  // S of the lines without a done env (the rest after B4)
-        obs_lines(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+      if (WAB_WIDE_ROLL_LINES && !WAB_WIDE_S_AFTER_B1)  // S of the lines without a done env (the rest after B4)
+        (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
       // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
       if (active && !job) {
@@ -1389,10 +1464,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       }
       lds_barrier();  // B1
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
+      if (WAB_WIDE_ROLL_LINES && WAB_WIDE_S_AFTER_B1) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid - 64);
       if (wave < 3 && !WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
-      if (WAB_WIDE_ROLL_LINES)
-        obs_lines(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+      if (WAB_WIDE_ROLL_LINES && !WAB_WIDE_S_AFTER_B1)
+        (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
     }
 
@@ -1485,8 +1561,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food2;
         }
       }
-      if (WAB_WIDE_ROLL_LINES)  // the lines that touch a done env: its new episode, its neighbours' S
-        obs_lines(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
+      if (WAB_WIDE_ROLL_LINES && WAB_WIDE_S_AFTER_B1) {  // the done envs' rows, by their S writers
+        if (wave > 0) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid - 64);
+      } else if (WAB_WIDE_ROLL_LINES) {  // the lines that touch a done env: its new episode, its neighbours' S
+        (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
+      }
       else
         for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
     }
