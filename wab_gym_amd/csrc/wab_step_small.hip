@@ -437,6 +437,9 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
 #ifndef WAB_ROLL_STORE_W3
 #define WAB_ROLL_STORE_W3 0
 #endif
+#ifndef WAB_ROLL_ALIGN  // multi-step launches: obs store instructions on absolute line boundaries (A/B)
+#define WAB_ROLL_ALIGN 0
+#endif
 // multi-step launches: obs stores non-temporal (1) or plain (0) (A/B)
 #ifndef WAB_ROLL_NT
 #define WAB_ROLL_NT 1
@@ -451,22 +454,27 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
   const uint32_t full = ((uint32_t)min((int64_t)64, p.B - g0) * OB) >> 4;
   uint8_t* out = planes + (size_t)g0 * OB;
   uint16_t* s16 = reinterpret_cast<uint16_t*>(stream);
+  // WAB_ROLL_ALIGN: units shifted by the group's offset within its first 128-byte line (OB odd:
+  // every other group starts mid-line), so that each 64-unit store instruction covers whole
+  // absolute lines; NT * NK - 7 still covers every unit (<= 1532 for odd OB <= 383)
+  const int sh = WAB_ROLL_ALIGN ? (int)((reinterpret_cast<uintptr_t>(out) & 127u) >> 4) : 0;
   uint32_t v[NK];
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
-    v[k] = u < full ? (uint32_t)s16[u] : 0u;
+    const int u = idx + NT * k - sh;
+    v[k] = u >= 0 && (uint32_t)u < full ? (uint32_t)s16[u] : 0u;
   }
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
-    if (u < full) s16[u] = 0;
+    const int u = idx + NT * k - sh;
+    if (u >= 0 && (uint32_t)u < full) s16[u] = 0;
   }
   if (!planes) return;  // (wab_rollout_features without planes: the stream is only cleared)
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    const uint32_t u = (uint32_t)idx + (uint32_t)NT * (uint32_t)k;
-    if (u >= full) break;
+    const int u = idx + NT * k - sh;
+    if (u >= 0 && (uint32_t)u >= full) break;
+    if (u < 0) continue;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     u32x4 q;
 #pragma unroll
