@@ -323,6 +323,10 @@ def test_rollout_equals_step_loop():
     ({"restrict_view": True, "lookout_only": False}, {"wolf_slots": 16}),
     (None, {"autoreset": False}),
     ({"starting_food": None, "starting_role": None}, {}),
+    # berries on every tile, two per bush: the ostrich eats nearly every turn and empties tiles
+    # (long eaten logs: entries >= 4 in HBM; emptied tiles scrolling back into view)
+    ({"bush_power": 1, "max_berries_per_bush": 2, "max_turns": 120}, {"eaten_capacity": 40}),
+    ({"bush_power": 1, "max_berries_per_bush": 3}, {"eaten_capacity": 3}),  # log overflow
 ])
 def test_rollout_variants_equal_step_loop(opts, kw):
     """wab_rollout == T wab_step calls, bit for bit, over two consecutive rollouts (state carried
@@ -835,6 +839,9 @@ def test_rollout_features_full_size_c5():
     ({"width": 31, "height": 15, "wolves_can_move": False, "god_mode": True}, 16, 8, True),
     ({"width": 13, "height": 11, "turns_to_fill_food": 4, "max_turns": 60, "bush_power": 60}, 16, 8, True),
     ({"width": 31, "height": 31}, 32, 16, False),                     # stepping past done
+    # eats nearly every turn, two berries per bush: eaten logs past the 16 kept on chip
+    ({"width": 31, "height": 31, "bush_power": 1, "max_berries_per_bush": 2, "max_turns": 120}, 32, 16, True),
+    ({"width": 25, "height": 25, "bush_power": 1, "max_berries_per_bush": 3}, 32, 8, True),
 ])
 def test_wide_rollout_equals_step_loop(opts, stride, slots, autoreset):
     """wab_rollout on the wide kernel (one launch of T steps, state carried on chip) == T wab_step
@@ -845,6 +852,8 @@ def test_wide_rollout_equals_step_loop(opts, stride, slots, autoreset):
     B, T = 1000, 45
     rs = np.random.RandomState(13)
     kw = dict(validate_actions=False, plane_stride=stride, wolf_slots=slots, autoreset=autoreset)
+    if opts.get("bush_power") == 1:
+        kw["eaten_capacity"] = 40 if opts.get("max_turns") else 3  # (3: the log overflows)
     e1, e2 = _env(opts, B, **kw), _env(opts, B, **kw)
     assert e1.step_kernel == "wide"
     e1.reset()
@@ -860,6 +869,25 @@ def test_wide_rollout_equals_step_loop(opts, stride, slots, autoreset):
     s1, s2 = e1.state(), e2.state()
     for k in s1:
         assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
+    assert e1.counters() == e2.counters()
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_rollout_tiny_batch(wide):
+    """A batch smaller than one 64-env group (16 envs), both rollout builds."""
+    import torch
+
+    opts = {"width": 31, "height": 31} if wide else None
+    kw = dict(validate_actions=False, plane_stride=32) if wide else dict(validate_actions=False)
+    e1, e2 = _env(opts, 16, **kw), _env(opts, 16, **kw)
+    e1.reset()
+    e2.reset()
+    a = torch.as_tensor(np.random.RandomState(5).randint(5, size=(50, 16)))
+    planes, scal, rew, done = e1.rollout(a)
+    for t in range(50):
+        e2.step(a[t])
+        assert torch.equal(planes[t], e2._obs["planes"]), t
+        assert torch.equal(rew[t], e2.reward), t
     assert e1.counters() == e2.counters()
 
 

@@ -62,6 +62,8 @@ def main():
     if args.b2b:
         return b2b_report(env, L, g, args.steps, args.b2b, args.graph)
     if args.rollout:
+        if env.step_kernel == "wide":
+            return rollout_wide_report(env, st, g, args.steps, args.rollout)
         return rollout_report(env, st, g, args.steps, args.rollout)
     if kind == "small":
         return small_report(env, st, g, args.steps)
@@ -226,6 +228,41 @@ def b2b_report(env, L, g, steps, n, graph=False):
     print("previous last end -> first entry (us):", us(gaps))
     if karg:
         print("entry -> first kernel-argument field by XCC (us):", us(karg))
+
+
+def rollout_wide_report(env, st, g, launches, T):
+    """wab_rollout_wide: the middle step's stamps of each wave (ROLLW_STAMP slots), averaged over
+    workgroups and launches; times from the step's first stamp."""
+    import numpy as np
+    import torch
+
+    B = env.num_envs
+    nb = (B + 63) // 64
+    seqs = {"W0": [0, 1, 2, 3, 4, 5, 6, 7], "W1": [8, 9, 10, 11, 12, 13], "W2": [16, 17, 18, 19, 20],
+            "W3": [24, 26, 27, 28], "jobs (W0)": [37, 39]}
+    names = {"W0": ["start", "despawn/pursuit/grid", "emptied clear + log -> B1", "after B1", "eat/done -> B2",
+                    "after B2", "S rows stored", "P2 (spawns, state)"],
+             "W1": ["start", "scroll (flag)", "tile value", "after B1", "after B2", "S rows stored"],
+             "W2": ["start", "spawn set", "after B1", "after B2", "S rows stored"],
+             "W3": ["start", "after B1", "after B2", "S rows stored"],
+             "jobs (W0)": ["after B4", "new-episode obs stored"]}
+    acc = {k: [] for k in seqs}
+    for it in range(launches):
+        st.zero_()
+        a = torch.randint(0, env.n_actions, (T, B), device="cuda:0", generator=g).to(torch.int8)
+        env.rollout(a)
+        torch.cuda.synchronize()
+        if it < 3:
+            continue
+        s = st.cpu().numpy().astype(np.int64)[:nb]
+        t0 = s[:, [0, 8, 16, 24]].min(axis=1)
+        for k, cols in seqs.items():
+            v = s[:, cols]
+            ok = (v > 0).all(axis=1)
+            acc[k].append((v[ok] - t0[ok, None]).mean(axis=0))
+    for k in seqs:
+        a = np.mean(acc[k], axis=0) * 10 / 1000
+        print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
 
 
 def rollout_report(env, st, g, launches, T):

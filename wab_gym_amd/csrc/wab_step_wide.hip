@@ -993,6 +993,19 @@ __device__ __forceinline__ void obs_rows_b1(const Params& p, const uint32_t* bm,
 #define WAB_WIDE_S_AFTER_B1 0
 #endif
 
+// Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
+// (tools/phase_stamps.py --rollout T --config wide31): W0 0..7, W1 8..13, W2 16..20, W3 24..27,
+// the done-env section 36..39
+#ifdef WAB_STAMPS
+#define ROLLW_STAMP(slot)                                                                \
+  do {                                                                                   \
+    if (lane == 0 && p.stamps && t == T / 2)                                             \
+      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#else
+#define ROLLW_STAMP(slot) do {} while (0)
+#endif
+
 #ifndef WAB_WIDE_ROW_STORES  // 1: obs_rows, 0: obs_lines (A/B)
 #define WAB_WIDE_ROW_STORES 1
 #endif
@@ -1097,6 +1110,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     unsigned long long eaten_of = 0, wolf_of = 0;
     uint32_t spill_live = 0;
 
+    ROLLW_STAMP(8 * wave);
     if (wave == 0) {
       // ------------------------------------------------ W0 P0: (loads,) despawn, pursuit, kill, wolf grid
       __builtin_amdgcn_s_setprio(3);
@@ -1201,6 +1215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         __builtin_amdgcn_wave_barrier();
         obs_plane<0>(p, wp, out, (uint32_t)n_active, lane);
       }
+      ROLLW_STAMP(1);
       // emptied tiles that scrolled back into view are absent from S (:506): cleared from the
       // bitmap once W1 has scrolled it (the per-step kernel's W1 does this from its own loads)
       const bool clear = active && ndep > 0 && h.dir != DIR_STAY;
@@ -1225,7 +1240,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (k < ne && lxy[k] == h.cpos) { found = k; found_rem = (int)lrem[k]; }
+      ROLLW_STAMP(2);
       lds_barrier();  // B1
+      ROLLW_STAMP(3);
       // ------------------------------------------------ W0 P1: eat, starve, done; then obs
       double reward = 0.0;
       if (active) {
@@ -1308,10 +1325,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       }
       __builtin_amdgcn_s_setprio(0);
       if (!WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
+      ROLLW_STAMP(4);
       lds_barrier();  // B2
+      ROLLW_STAMP(5);
       if (WAB_WIDE_ROLL_LINES && !WAB_WIDE_S_AFTER_B1)  // S of the lines without a done env (the rest after B4)
         (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
+      ROLLW_STAMP(6);
       // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
       if (active && !job) {
         int n_unplaced = 0;
@@ -1436,6 +1456,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) lds_publish_step(flag, (uint32_t)t + 1u);  // (W0 clears the emptied tiles)
+        ROLLW_STAMP(9);
         uint32_t cv = 0;  // the generated berries of the ostrich's tile (:631-635), for W0 (unused
                           // when W0 clears that tile: it is then in the log with no berries)
         if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
@@ -1443,6 +1464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
                                          p.bush_power);
         cval[lane] = cv;
         __builtin_amdgcn_s_setprio(0);
+        ROLLW_STAMP(10);
       } else {
         // ---------------------------------------------- W3: ostrich grids; W2: tables, spawn set
         if (wave == 3 && !WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
@@ -1460,18 +1482,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
               spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
             });
           if (!WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
+          ROLLW_STAMP(17);
         }
       }
       lds_barrier();  // B1
+      ROLLW_STAMP(8 * wave + (wave == 1 ? 3 : 2));
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
       if (WAB_WIDE_ROLL_LINES && WAB_WIDE_S_AFTER_B1) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid - 64);
       if (wave < 3 && !WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
+      ROLLW_STAMP(8 * wave + (wave == 1 ? 4 : 3));
       if (WAB_WIDE_ROLL_LINES && !WAB_WIDE_S_AFTER_B1)
         (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
+      ROLLW_STAMP(8 * wave + (wave == 1 ? 5 : 4));
     }
 
+    if (wave == 0) ROLLW_STAMP(7);
     const int n_jobs = (int)blk[0];
     const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
     // ------------------------------------------------ P2: the continuing envs' bitmaps (post-eat)
@@ -1512,6 +1539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
                      });
       }
       lds_barrier();  // B4
+      if (wave == 0) ROLLW_STAMP(37);
       if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
         // spawn_ostriches (:595-611) and the initial wolves, one per wolf cell of the view
         const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
@@ -1569,6 +1597,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       else
         for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
     }
+    if (wave == 0) ROLLW_STAMP(39);
     if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     if (last) {  // every env's bitmap rows (continuing: post-eat; done: the new episode's)
       lds_barrier();
