@@ -1,0 +1,10 @@
+# wide rollout: W3 draws the entering strip for W1 (A/B), parity, stamps
+set -e
+o=gpurun_out/s2o
+mkdir -p $o
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "wide_rollout or tiny" -x -q --timeout 300 --timeout-method thread > $o/wide_roll_tests.log 2>&1
+for r in 1 2; do for v in st3 st1; do
+WAB_LIB=wab_gym_amd/_lib/var/lib_$v.so timeout -k 10 200 python bench.py --config wide31 --no-cpu --steps 640 > $o/ab_${v}_$r.log 2>&1
+python -c "import json; d=json.loads(open('$o/ab_${v}_$r.log').read().strip().splitlines()[-1]); print('$v', $r, d['ms_per_step'] * 1e3)"
+done; done > $o/ab_wide.log
+timeout -k 10 300 python tools/phase_stamps.py --no-build --config wide31 --rollout 32 --steps 12 > $o/wide_roll_stamps.log 2>&1

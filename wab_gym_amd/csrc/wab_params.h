@@ -220,6 +220,7 @@ struct WideLayout {
   uint32_t bm, wp, spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey;
   uint32_t nhdr, act, flag;  // multi-step launches: next headers (W0), next actions, W1 -> W0 flag
   uint32_t elxy, elrem;      // multi-step launches: eaten-log entries 4..kWideLdsLog-1 (W0)
+  uint32_t wstrip;           // multi-step launches: the entering strip's bits (W3 -> W1)
   uint32_t total;
 };
 
@@ -245,6 +246,7 @@ __host__ __device__ inline WideLayout wide_layout(const Params& p) {
   L.flag = o; o += 4u;
   L.elxy = o; o += 64u * (uint32_t)(kWideLdsLog - 4);      // [entry - 4][env] tiles
   L.elrem = o; o += 16u * (uint32_t)(kWideLdsLog - 4);     // [entry - 4][env] berries left (bytes)
+  L.wstrip = o; o += 64u;
   L.total = o;
   return L;
 }

@@ -437,6 +437,9 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
 #ifndef WAB_ROLL_STORE_W3
 #define WAB_ROLL_STORE_W3 0
 #endif
+#ifndef WAB_ROLL_STORE_BATCH  // multi-step launches: obs units per read/clear/store batch (A/B)
+#define WAB_ROLL_STORE_BATCH 12
+#endif
 #ifndef WAB_ROLL_ALIGN  // multi-step launches: obs store instructions on absolute line boundaries (A/B)
 #define WAB_ROLL_ALIGN 0
 #endif
@@ -458,29 +461,34 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
   // every other group starts mid-line), so that each 64-unit store instruction covers whole
   // absolute lines; NT * NK - 7 still covers every unit (<= 1532 for odd OB <= 383)
   const int sh = WAB_ROLL_ALIGN ? (int)((reinterpret_cast<uintptr_t>(out) & 127u) >> 4) : 0;
-  uint32_t v[NK];
+  // in batches of KB units (all read, then cleared, then expanded and stored): fewer live
+  // registers than one batch of NK (WAB_ROLL_STORE_BATCH)
+  constexpr int KB = WAB_ROLL_STORE_BATCH < NK ? WAB_ROLL_STORE_BATCH : NK;
 #pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int u = idx + NT * k - sh;
-    v[k] = u >= 0 && (uint32_t)u < full ? (uint32_t)s16[u] : 0u;
-  }
+  for (int k0 = 0; k0 < NK; k0 += KB) {
+    uint32_t v[KB];
 #pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int u = idx + NT * k - sh;
-    if (u >= 0 && (uint32_t)u < full) s16[u] = 0;
-  }
-  if (!planes) return;  // (wab_rollout_features without planes: the stream is only cleared)
+    for (int k = 0; k < KB; ++k) {
+      const int u = idx + NT * (k0 + k) - sh;
+      v[k] = k0 + k < NK && u >= 0 && (uint32_t)u < full ? (uint32_t)s16[u] : 0u;
+    }
 #pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int u = idx + NT * k - sh;
-    if (u >= 0 && (uint32_t)u >= full) break;
-    if (u < 0) continue;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 q;
+    for (int k = 0; k < KB; ++k) {
+      const int u = idx + NT * (k0 + k) - sh;
+      if (k0 + k < NK && u >= 0 && (uint32_t)u < full) s16[u] = 0;
+    }
+    if (!planes) continue;  // (wab_rollout_features without planes: the stream is only cleared)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    if (WAB_ROLL_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
-    else reinterpret_cast<u32x4*>(out)[u] = q;
+    for (int k = 0; k < KB; ++k) {
+      const int u = idx + NT * (k0 + k) - sh;
+      if (k0 + k >= NK || u < 0 || (uint32_t)u >= full) continue;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 q;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
+      if (WAB_ROLL_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+      else reinterpret_cast<u32x4*>(out)[u] = q;
+    }
   }
 }
 

@@ -1006,6 +1006,10 @@ __device__ __forceinline__ void obs_rows_b1(const Params& p, const uint32_t* bm,
 #define ROLLW_STAMP(slot) do {} while (0)
 #endif
 
+#ifndef WAB_WIDE_STRIP_W3  // multi-step launches: W3 draws the entering strip for W1 (A/B)
+#define WAB_WIDE_STRIP_W3 1
+#endif
+
 #ifndef WAB_WIDE_ROW_STORES  // 1: obs_rows, 0: obs_lines (A/B)
 #define WAB_WIDE_ROW_STORES 1
 #endif
@@ -1049,9 +1053,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   uint32_t live = 0;  // occupied register slots
   int nsp = 0;        // wolves in HBM rows SLOTS..SLOTS+nsp-1
   uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
-  {  // the W1 -> W0 step flag starts below every step's value
+  {  // the W1 -> W0 and W3 -> W1 step flags start below every step's value
     const WideLayout L = wide_layout(p0);
-    if (tid == 0) lds[L.flag] = 0u;
+    if (tid == 0) {
+      lds[L.flag] = 0u;
+      lds[L.flag + 1] = 0u;
+    }
     lds_barrier();
   }
 
@@ -1074,16 +1081,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     uint4* nhdr = reinterpret_cast<uint4*>(lds + L.nhdr);
     uint32_t* act = lds + L.act;
     uint32_t* flag = lds + L.flag;
+    uint32_t* wstrip = lds + L.wstrip;
     uint32_t* elxy = lds + L.elxy;
     uint8_t* elrem = reinterpret_cast<uint8_t*>(lds + L.elrem);
-    // eaten-log entry i >= 4 of this lane's env: LDS below kWideLdsLog, else HBM (rare; a load
-    // there waits for this wave's outstanding stores)
-    auto log_xy = [&](int i) -> uint32_t {
-      return i < kWideLdsLog ? elxy[(i - 4) * 64 + lane] : p.eaten_xy[(int64_t)i * p.B + g];
-    };
-    auto log_rem = [&](int i) -> uint32_t {
-      return i < kWideLdsLog ? (uint32_t)elrem[(i - 4) * 64 + lane] : (uint32_t)p.eaten_rem[(int64_t)i * p.B + g];
-    };
+    // (eaten-log entries 4..kWideLdsLog-1 in LDS, later ones in HBM: rare, a load there waits
+    // for this wave's outstanding stores)
     const uint32_t OB = (uint32_t)p.OB;
     uint8_t* out = p.planes + (size_t)g0 * OB;
     const int RW = (p.R + 31) >> 5;
@@ -1094,6 +1096,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         hdr = p.hdr[g];
         a = (int)p.actions[g];
       }
+      // (every step-0 load settled inside its branch: the waitcnt pass would otherwise put
+      // vmcnt(0) waits at the join that every later step executes too, each one waiting for all
+      // of the wave's obs stores in flight)
+      __builtin_amdgcn_s_waitcnt(0);
     } else {
       hdr = nhdr[lane];
       a = (int)reinterpret_cast<const int8_t*>(act)[lane];
@@ -1132,6 +1138,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             elrem[(i - 4) * 64 + lane] = p.eaten_rem[(int64_t)i * p.B + g];
           }
         }
+        __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int k = 0; k < SLOTS; ++k) opaque(wr[k]);
         opaque(food);
@@ -1228,11 +1235,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             if (k < ne && lrem[k] == 0u && abs(ddx) <= p.cw && abs(ddy) <= p.ch)
               bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
           }
-          for (int i = 4; i < ne; ++i) {  // (more than 4 eaten tiles this episode)
-            if (log_rem(i) != 0u) continue;
-            const uint32_t tt = log_xy(i);
+          for (int i = 4; i < ne && i < kWideLdsLog; ++i) {  // (more than 4 eaten tiles: LDS)
+            if (elrem[(i - 4) * 64 + lane] != 0u) continue;
+            const uint32_t tt = elxy[(i - 4) * 64 + lane];
             const int ddx = h.ox - xy_x(tt), ddy = h.oy - xy_y(tt);
             if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+          }
+          if (ne > kWideLdsLog) {  // (rare: the rest in HBM; a load here waits for the stores)
+            for (int i = kWideLdsLog; i < ne; ++i) {
+              if (p.eaten_rem[(int64_t)i * p.B + g] != 0) continue;
+              const uint32_t tt = p.eaten_xy[(int64_t)i * p.B + g];
+              const int ddx = h.ox - xy_x(tt), ddy = h.oy - xy_y(tt);
+              if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
+            }
           }
         }
       }
@@ -1248,8 +1263,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       if (active) {
         const bool center_bush = ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u) != 0u;
         if (center_bush && found < 0 && ne > 4) {
-          for (int i = 4; i < ne; ++i)
-            if (log_xy(i) == h.cpos) { found = i; found_rem = (int)log_rem(i); }
+          for (int i = 4; i < ne && i < kWideLdsLog; ++i)
+            if (elxy[(i - 4) * 64 + lane] == h.cpos) { found = i; found_rem = (int)elrem[(i - 4) * 64 + lane]; }
+          if (ne > kWideLdsLog)  // (rare)
+            for (int i = kWideLdsLog; i < ne; ++i)
+              if (p.eaten_xy[(int64_t)i * p.B + g] == h.cpos) { found = i; found_rem = (int)p.eaten_rem[(int64_t)i * p.B + g]; }
         }
         const int rem = found >= 0 ? found_rem : (center_bush ? (int)cval[lane] : 0);
         if (rem > 0 && status_old == 0 && (h.role == 1 || p.lookout_only)) {  // eat (:299-313)
@@ -1404,7 +1422,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       if (wave == 1) {
         // ---------------------------------------------- W1 P0: the view bitmap
         __builtin_amdgcn_s_setprio(2);
-        uint32_t w[32];
+        // (the view bitmap is scrolled in place in LDS, a few rows at a time: a 32-row register
+        // copy set the whole kernel's register budget, and its spills to scratch are vector
+        // loads that wait for every obs store this wave has in flight)
         if (t == 0) {
           const int nthr = p.max_berries;
           uint64_t tv[4];
@@ -1412,46 +1432,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
           const int64_t ga = active ? g : 0;
           const uint4* src = reinterpret_cast<const uint4*>(p.bushmap + (size_t)ga * 32u);
+#pragma unroll 1
+          for (int k = 0; k < 8; k += 2) {  // (step 0 only)
+            const uint4 v0 = src[k], v1 = src[k + 1];
+            const uint32_t r[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint4 v = src[k];
-            w[4 * k] = v.x;
-            w[4 * k + 1] = v.y;
-            w[4 * k + 2] = v.z;
-            w[4 * k + 3] = v.w;
+            for (int q = 0; q < 8; ++q)
+              if (4 * k + q < p.W) bm[me + (uint32_t)(4 * k + q)] = r[q];
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
           if (lane == 0) bush_thr_pads(thr, nthr);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 32; ++i) w[i] = i < p.W ? bm[me + (uint32_t)i] : 0u;
-          if (WAB_WIDE_ROLL_LINES) {  // the last step's eaten-empty tile (its S obs are stored)
-            const unsigned long long jmp = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
-            if (lane < n_active && !((jmp >> lane) & 1ull) && (info[lane] & 2u)) {
-#pragma unroll
-              for (int i = 0; i < 32; ++i)
-                if (i == p.cw) w[i] &= ~(1u << p.ch);
-            }
-          }
+          __builtin_amdgcn_s_waitcnt(0);
+        } else if (WAB_WIDE_ROLL_LINES) {  // the last step's eaten-empty tile (its S obs are stored)
+          const unsigned long long jmp = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+          if (lane < n_active && !((jmp >> lane) & 1ull) && (info[lane] & 2u))
+            bm[me + (uint32_t)p.cw] &= ~(1u << p.ch);
         }
-        const uint32_t strip = active ? strip_bits(p, h) : 0u;
+        uint32_t strip;
+        if (WAB_WIDE_STRIP_W3) {  // drawn by W3 meanwhile (flag[1] = t + 1)
+          lds_await_step(p, flag + 1, (uint32_t)t + 1u);
+          strip = wstrip[lane];
+        } else {
+          strip = active ? strip_bits(p, h) : 0u;
+        }
         const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
         const uint32_t top = 1u << (p.H - 1);
+        const int Wv = p.W;
+        uint32_t prev_old = 0u;             // the old row i - 1
+        uint32_t nxt = active ? bm[me] : 0u;  // the old row i
+#pragma unroll 1
+        for (int i0 = 0; i0 < Wv; i0 += 4) {  // scroll (:613-629) + the entering strip, in place
+          uint32_t old[5];
+          old[0] = nxt;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {  // scroll (:613-629) + the entering strip
-          if (i >= p.W) break;
-          const uint32_t wi = active ? w[i] : 0u;
-          const uint32_t prev = (active && i > 0) ? w[i - 1] : 0u;
-          const uint32_t next = (active && i < 31 && i + 1 < p.W) ? w[i + 1] : 0u;
-          const uint32_t sb = (strip >> i) & 1u;
-          uint32_t v = wi;
-          v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
-          v = h.dir == DIR_LEFT ? (i == p.W - 1 ? strip : next) : v;
-          v = h.dir == DIR_UP ? (((wi << 1) & hmask) | sb) : v;
-          v = h.dir == DIR_DOWN ? ((wi >> 1) | (sb ? top : 0u)) : v;
-          bm[me + (uint32_t)i] = v;
+          for (int q = 1; q < 5; ++q) old[q] = (active && i0 + q < Wv) ? bm[me + (uint32_t)(i0 + q)] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = i0 + q;
+            if (i >= Wv) break;
+            const uint32_t wi = old[q];
+            const uint32_t prev = q == 0 ? prev_old : old[q - 1];
+            const uint32_t next = old[q + 1];
+            const uint32_t sb = (strip >> i) & 1u;
+            uint32_t v = wi;
+            v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
+            v = h.dir == DIR_LEFT ? (i == Wv - 1 ? strip : next) : v;
+            v = h.dir == DIR_UP ? (((wi << 1) & hmask) | sb) : v;
+            v = h.dir == DIR_DOWN ? ((wi >> 1) | (sb ? top : 0u)) : v;
+            bm[me + (uint32_t)i] = active ? v : 0u;
+          }
+          prev_old = old[3];
+          nxt = old[4];
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
@@ -1467,12 +1500,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         ROLLW_STAMP(10);
       } else {
         // ---------------------------------------------- W3: ostrich grids; W2: tables, spawn set
+        if (wave == 3 && WAB_WIDE_STRIP_W3) {  // the entering strip's draws, for W1's scroll
+          wstrip[lane] = active ? strip_bits(p, h) : 0u;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) lds_publish_step(flag + 1, (uint32_t)t + 1u);
+        }
         if (wave == 3 && !WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
         if (wave == 2) {
           if (t == 0) {
             copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
             if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_waitcnt(0);
           }
           for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
