@@ -992,6 +992,11 @@ __device__ __forceinline__ void obs_rows_b1(const Params& p, const uint32_t* bm,
 #ifndef WAB_WIDE_S_AFTER_B1  // 1: obs_rows_b1 after B1 and for the done envs after B4 (A/B)
 #define WAB_WIDE_S_AFTER_B1 0
 #endif
+// 1: the workgroups of every other 256-block (which share CUs with the others) store S after
+// B1, the rest after B2, so that the workgroups of a CU do not all store at once (A/B)
+#ifndef WAB_WIDE_S_MIX
+#define WAB_WIDE_S_MIX 0
+#endif
 
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
 // (tools/phase_stamps.py --rollout T --config wide31): W0 0..7, W1 8..13, W2 16..20, W3 24..27,
@@ -1038,6 +1043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   if (g0 >= p0.B) return;  // (uniform over the workgroup)
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int T = p0.n_steps;
+  const bool s_b1 = WAB_WIDE_S_AFTER_B1 || (WAB_WIDE_S_MIX && ((blockIdx.x >> 8) & 1u));  // (uniform)
   const int n_active = (int)min((int64_t)64, p0.B - g0);
   const int64_t g = g0 + lane;
   const bool active = lane < n_active;
@@ -1346,7 +1352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       ROLLW_STAMP(4);
       lds_barrier();  // B2
       ROLLW_STAMP(5);
-      if (WAB_WIDE_ROLL_LINES && !WAB_WIDE_S_AFTER_B1)  // S of the lines without a done env (the rest after B4)
+      if (WAB_WIDE_ROLL_LINES && !s_b1)  // S of the lines without a done env (the rest after B4)
         (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
       ROLLW_STAMP(6);
@@ -1527,11 +1533,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       lds_barrier();  // B1
       ROLLW_STAMP(8 * wave + (wave == 1 ? 3 : 2));
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
-      if (WAB_WIDE_ROLL_LINES && WAB_WIDE_S_AFTER_B1) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid - 64);
+      if (WAB_WIDE_ROLL_LINES && s_b1) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid - 64);
       if (wave < 3 && !WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
       ROLLW_STAMP(8 * wave + (wave == 1 ? 4 : 3));
-      if (WAB_WIDE_ROLL_LINES && !WAB_WIDE_S_AFTER_B1)
+      if (WAB_WIDE_ROLL_LINES && !s_b1)
         (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
                   false, tid);
       ROLLW_STAMP(8 * wave + (wave == 1 ? 5 : 4));
@@ -1628,7 +1634,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food2;
         }
       }
-      if (WAB_WIDE_ROLL_LINES && WAB_WIDE_S_AFTER_B1) {  // the done envs' rows, by their S writers
+      if (WAB_WIDE_ROLL_LINES && s_b1) {  // the done envs' rows, by their S writers
         if (wave > 0) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid - 64);
       } else if (WAB_WIDE_ROLL_LINES) {  // the lines that touch a done env: its new episode, its neighbours' S
         (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
