@@ -1542,6 +1542,21 @@ __device__ __forceinline__ void step_slice(Params& p, int t) {
   if (p.features) p.features += o * pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
 }
 
+// Multi-step launches (A/B, WAB_ROLL_STAGGER_NS > 0): the four workgroups that share a CU
+// (blockIdx 256 apart) start their first step k * STAGGER ns apart, k = blockIdx >> 8 & 3, so
+// that their store phases do not coincide (they otherwise stay in phase: they share one drain)
+#ifndef WAB_ROLL_STAGGER_NS
+#define WAB_ROLL_STAGGER_NS 0
+#endif
+__device__ __forceinline__ void roll_stagger() {
+  if (WAB_ROLL_STAGGER_NS > 0) {
+    const uint64_t k = (blockIdx.x >> 8) & 3u;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    const uint64_t until = t0 + k * (uint64_t)(WAB_ROLL_STAGGER_NS / 10);
+    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 template <int SLOTS, int G, bool FEAT, bool ROLL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 1))) void wab_step_small(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1595,6 +1610,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     // depend on nothing outside it), each wave's state carried in registers from step to step
     // (see CarryW0): one barrier closes a step (its LDS is reused by the next)
     const int T = p0.n_steps;
+    roll_stagger();
     {  // the second stream starts clear (the first is cleared by W0 in step 0)
       const SmallLayout L = small_layout(p0);
       uint4* z = reinterpret_cast<uint4*>(lds + L.stream2);

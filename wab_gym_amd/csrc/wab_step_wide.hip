@@ -1036,6 +1036,21 @@ __device__ __forceinline__ void wide_step_slice(Params& p, int t) {
 
 }  // namespace
 
+// Multi-step launches (A/B, WAB_ROLL_STAGGER_NS > 0): the four workgroups that share a CU
+// (blockIdx 256 apart) start their first step k * STAGGER ns apart, k = blockIdx >> 8 & 3, so
+// that their store phases do not coincide (they otherwise stay in phase: they share one drain)
+#ifndef WAB_ROLL_STAGGER_NS
+#define WAB_ROLL_STAGGER_NS 0
+#endif
+__device__ __forceinline__ void roll_stagger() {
+  if (WAB_ROLL_STAGGER_NS > 0) {
+    const uint64_t k = (blockIdx.x >> 8) & 3u;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    const uint64_t until = t0 + k * (uint64_t)(WAB_ROLL_STAGGER_NS / 10);
+    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 template <int SLOTS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wab_rollout_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1043,6 +1058,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   if (g0 >= p0.B) return;  // (uniform over the workgroup)
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int T = p0.n_steps;
+  roll_stagger();
   const bool s_b1 = WAB_WIDE_S_AFTER_B1 || (WAB_WIDE_S_MIX && ((blockIdx.x >> 8) & 1u));  // (uniform)
   const int n_active = (int)min((int64_t)64, p0.B - g0);
   const int64_t g = g0 + lane;
