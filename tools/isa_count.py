@@ -13,7 +13,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "wab_gym_amd", "csrc", "wab_step_small.hip")
-KERNEL = "_ZN3wab14wab_step_smallILi8ELi11ELb0ELb0EEEvNS_6ParamsE"
+KERNEL = os.environ.get("ISA_KERNEL", "_ZN3wab14wab_step_smallILi8ELi11ELb0ELb0EEEvNS_6ParamsE")
 
 
 def counts(flags):

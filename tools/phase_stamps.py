@@ -28,6 +28,8 @@ def main():
                     help="instead: per-XCD entry/end of the last two of N back-to-back launches")
     ap.add_argument("--rollout", type=int, default=0,
                     help="instead: per-wave phases of the middle step of T-step wab_rollout launches")
+    ap.add_argument("--features", action="store_true",
+                    help="with --rollout: wab_rollout_features launches (C5), plus the feature emit and row stores")
     ap.add_argument("--graph", action="store_true",
                     help="with --b2b: the N launches captured in a graph and replayed (the bench's shape)")
     args = ap.parse_args()
@@ -64,7 +66,7 @@ def main():
     if args.rollout:
         if env.step_kernel == "wide":
             return rollout_wide_report(env, st, g, args.steps, args.rollout)
-        return rollout_report(env, st, g, args.steps, args.rollout)
+        return rollout_report(env, st, g, args.steps, args.rollout, args.features)
     if kind == "small":
         return small_report(env, st, g, args.steps)
     if kind == "wide":
@@ -265,7 +267,7 @@ def rollout_wide_report(env, st, g, launches, T):
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
 
 
-def rollout_report(env, st, g, launches, T):
+def rollout_report(env, st, g, launches, T, features=False):
     """wab_rollout (the small kernel's multi-step build): the middle step's stamps of each wave
     (SMALL_STAMP slots as in small_report; step t > 0 has no loads and no B_init), averaged over
     workgroups and launches; times from the step's first stamp."""
@@ -282,15 +284,21 @@ def rollout_report(env, st, g, launches, T):
              "W3": ["start", "spawn set + strip -> B1", "reset draws", "await W1", "new episodes -> B2", "after B2"]}
     acc = {k: [] for k in seqs}
     spans = []
+    feats = torch.empty((T, B, 449), device="cuda:0") if features else None
     for it in range(launches):
         st.zero_()
         a = torch.randint(0, env.n_actions, (T, B), device="cuda:0", generator=g).to(torch.int8)
-        env.rollout(a)
+        if features:
+            env.rollout_features(a, features=feats)
+        else:
+            env.rollout(a)
         torch.cuda.synchronize()
         if it < 3:
             continue
         s = st.cpu().numpy().astype(np.int64)[:nb]
         t0 = s[:, [0, 10, 16, 22]].min(axis=1)
+        if features:
+            acc.setdefault("feat", []).append((s[:, [36, 37]] - t0[:, None]).mean(axis=0))
         for k, cols in seqs.items():
             v = s[:, cols]
             ok = (v > 0).all(axis=1)
@@ -300,6 +308,9 @@ def rollout_report(env, st, g, launches, T):
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
     print("step start -> last wave past B2 (mean over workgroups): %.2f us" % (np.mean(spans) * 10 / 1000))
+    if features:
+        f = np.mean(acc["feat"], axis=0) * 10 / 1000
+        print("features: emitted %.2f, wave 0's row stores issued %.2f us" % (f[0], f[1]))
 
 
 def small_report(env, st, g, steps):

@@ -1476,7 +1476,7 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
 #endif
 template <bool ROLL = false>
 __device__ __forceinline__ void step_features(const Params& p, const SmallLayout& L, uint32_t* lds, int wave,
-                                              int lane) {
+                                              int lane, int t = 0) {
   const int md = p.W / 2 + p.H / 2 + 1;
   const uint32_t F = (uint32_t)pragmatic_dim(md, p.turns_empty), WH = (uint32_t)p.WH;
   const int64_t g0 = (int64_t)blockIdx.x * 64;
@@ -1499,10 +1499,20 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
                    sc >> 16, p.restrict_view != 0, view_mask_of(p, (int)role));
     }
   }
+#ifdef WAB_STAMPS
+  const auto stamp = [&](int slot) {  // (multi-step launches: the middle step, wave 0)
+    if (ROLL && threadIdx.x == 0 && p.stamps && t == p.n_steps / 2)
+      p.stamps[(size_t)blockIdx.x * 40 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(36);  // the feature bits emitted
+#endif
   lds_barrier();
   constexpr bool NT = ROLL && WAB_ROLL_FEAT_NT;
   if (p.restrict_view || (ROLL && !WAB_ROLL_EARLY_VIEWS)) store_feature_bits<NT>(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
   else store_rows_skip_views<NT>(ob, p.features + (size_t)g0 * F, n_active * F, F, (int)threadIdx.x, 256);
+#ifdef WAB_STAMPS
+  stamp(37);  // wave 0's row stores issued
+#endif
 }
 
 }  // namespace
@@ -1638,7 +1648,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
       } else {                                                                               \
         __VA_ARGS__;                                                                         \
       }                                                                                      \
-      if (FEAT) step_features<true>(p, L, lds, wave, lane);  /* this step's rows */        \
+      if (FEAT) step_features<true>(p, L, lds, wave, lane, t);  /* this step's rows */     \
       if (WAB_ROLL_STORE == 1 && t > 0 && pp.planes) store_units_of<3, 6>(pp, prev, threadIdx.x); \
       if (WAB_ROLL_STORE == 0) {                                                             \
         if (p.planes) store_obs<true>(p, lds + L.stream, threadIdx.x);                       \
