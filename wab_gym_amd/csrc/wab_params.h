@@ -167,6 +167,7 @@ struct SmallLayout {
   uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
   uint32_t rcode;       // wab_rollout_features with returns: [n_steps][64] reward codes (bytes)
+  uint32_t fbits2;      // multi-step fused features: the odd steps' feature bits (rows stored a step later)
 };
 
 __host__ __device__ inline SmallLayout small_layout(const Params& p) {
@@ -203,6 +204,8 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
     L.fzero = o - L.fbits;
     L.scal = o; o += 64u;
   }
+  L.fbits2 = o;
+  if (p.features && p.n_steps > 1) o += lds_align4(((64u * (uint32_t)(16 * (p.W / 2 + p.H / 2 + 2) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121) + 31u) >> 5) + 4u);
   L.rcode = o;
   if (p.returns) o += 16u * (uint32_t)p.n_steps;  // one byte per env and step
   L.total = o;

@@ -437,6 +437,15 @@ __device__ __forceinline__ void store_units(const Params& p, const uint32_t* str
 #ifndef WAB_ROLL_STORE_W3
 #define WAB_ROLL_STORE_W3 0
 #endif
+// multi-step launches: each step's feature rows stored during the next step by W0 and W2 in
+// their slack before B2 (1; double-buffered feature bits), or by all threads at the step's end (0)
+#ifndef WAB_ROLL_FEAT_DEFER
+#define WAB_ROLL_FEAT_DEFER 0
+#endif
+// multi-step launches: feature rows non-temporal (1) or plain (0) (A/B)
+#ifndef WAB_ROLL_FEAT_NT
+#define WAB_ROLL_FEAT_NT 1
+#endif
 #ifndef WAB_ROLL_STORE_BATCH  // multi-step launches: obs units per read/clear/store batch (A/B)
 #define WAB_ROLL_STORE_BATCH 12
 #endif
@@ -490,6 +499,17 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
       else reinterpret_cast<u32x4*>(out)[u] = q;
     }
   }
+}
+
+// WAB_ROLL_FEAT_DEFER: the previous step's feature rows (its bits in the other buffer) by the
+// 128 threads of W0 and W2
+__device__ __forceinline__ void roll_feature_rows(const Params& p, const SmallLayout& L, const uint32_t* lds, int t,
+                                                  int idx) {
+  const uint32_t F = (uint32_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
+  const uint32_t* ob = lds + (((t - 1) & 1) ? L.fbits2 : L.fbits);
+  store_feature_bits<WAB_ROLL_FEAT_NT>(ob, p.features - (int64_t)p.B * F + (size_t)g0 * F, n_active * F, idx, 128);
 }
 
 // WAB_ROLL_STORE (A/B of the multi-step launch's obs stores): 0 every thread at the step's end
@@ -924,6 +944,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     if (WAB_ROLL_STORE_W3) store_units_nt<192, 8>(p, carry->prev_planes, carry->prev_stream, lane);
     else store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
   }
+  if (ROLL && WAB_ROLL_FEAT_DEFER && p.features && t > 0) roll_feature_rows(p, L, lds, t, lane);
   SMALL_STAMP(4);
   lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
   if (p.t_planes) {
@@ -1242,6 +1263,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
     if (WAB_ROLL_STORE_W3) store_units_nt<192, 8>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
     else store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
   }
+  if (ROLL && WAB_ROLL_FEAT_DEFER && p.features && t > 0) roll_feature_rows(p, L, lds, t, 64 + lane);
   SMALL_STAMP(19);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -1316,7 +1338,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   }
   if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned;
                      // multi-step launches: the tables once, the bits every step)
-    uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
+    uint4* z = reinterpret_cast<uint4*>(lds + (ROLL && WAB_ROLL_FEAT_DEFER && (t & 1) ? L.fbits2 : L.fbits));
     const uint32_t nz = ROLL && t > 0 ? L.ftab - L.fbits : L.fzero;
     for (uint32_t i = lane; i < nz / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
@@ -1470,10 +1492,6 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
 // from the rendered bit-stream (after B2, or B3) and the scalars each env's writer handed over:
 // W0 the wolf plane, W1 the bush plane, W2 the scalars and view mask, one more barrier, then
 // all 256 threads expand the feature bits to float32 (the featurizer's phases 2 and 3).
-// multi-step launches: feature rows non-temporal (1) or plain (0) (A/B)
-#ifndef WAB_ROLL_FEAT_NT
-#define WAB_ROLL_FEAT_NT 1
-#endif
 template <bool ROLL = false>
 __device__ __forceinline__ void step_features(const Params& p, const SmallLayout& L, uint32_t* lds, int wave,
                                               int lane, int t = 0) {
@@ -1482,7 +1500,7 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
   const uint32_t* stream = lds + L.stream;
-  uint32_t* ob = lds + L.fbits;
+  uint32_t* ob = lds + (ROLL && WAB_ROLL_FEAT_DEFER && (t & 1) ? L.fbits2 : L.fbits);
   if ((uint32_t)lane < n_active && wave < 3) {
     const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, at = (uint32_t)lane * F;
     if (wave <= 1) {  // W0 wolves, W1 bushes
@@ -1506,6 +1524,9 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   };
   stamp(36);  // the feature bits emitted
 #endif
+  // (WAB_ROLL_FEAT_DEFER: the rows of a step but the last are stored during the next step by W0
+  // and W2 in their slack before B2, roll_feature_rows; the step's end barrier orders the bits)
+  if (ROLL && WAB_ROLL_FEAT_DEFER && t != p.n_steps - 1) return;
   lds_barrier();
   constexpr bool NT = ROLL && WAB_ROLL_FEAT_NT;
   if (p.restrict_view || (ROLL && !WAB_ROLL_EARLY_VIEWS)) store_feature_bits<NT>(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
