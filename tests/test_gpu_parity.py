@@ -914,3 +914,39 @@ def test_wide_rollout_full_size_c3():
             assert torch.equal(scal[t], e2._obs["scalars"]), (seg, t)
         del planes
     assert e1.counters() == e2.counters()
+
+
+@pytest.mark.parametrize("wide", [False, True])
+@pytest.mark.parametrize("T", [1, 2, 3])
+def test_rollout_short_segments(wide, T):
+    """Rollouts of 1, 2 and 3 steps (the first step is also the last; one carried step) chained
+    five times, both rollout builds, == the step loop; C5's fused rollout too on the small view."""
+    import torch
+
+    from wab_gym_amd.wrappers import discounted_returns
+
+    opts = {"width": 31, "height": 31} if wide else None
+    kw = dict(validate_actions=False, plane_stride=32) if wide else dict(validate_actions=False)
+    B = 192
+    e1, e2 = _env(opts, B, **kw), _env(opts, B, **kw)
+    e1.reset()
+    e2.reset()
+    rs = np.random.RandomState(T)
+    for seg in range(5):
+        a = torch.as_tensor(rs.randint(5, size=(T, B)))
+        planes, scal, rew, done = e1.rollout(a)
+        for t in range(T):
+            e2.step(a[t])
+            assert torch.equal(planes[t], e2._obs["planes"]), (seg, t)
+            assert torch.equal(rew[t], e2.reward) and torch.equal(done[t].bool(), e2.done.bool()), (seg, t)
+    assert e1.counters() == e2.counters()
+    if not wide:
+        e3, e4 = _env(None, B, **kw), _env(None, B, **kw)
+        e3.reset()
+        e4.reset()
+        for seg in range(5):
+            a = torch.as_tensor(rs.randint(5, size=(T, B))).cuda()
+            r = e3.rollout_features(a)
+            feats, rw, dn, _, _ = _step_features_loop(e4, a, 449, False)
+            assert torch.equal(r["features"], feats) and torch.equal(r["reward"], rw), seg
+            assert torch.equal(r["returns"], discounted_returns(rw, dn, gamma=0.99, env=e4)), seg
