@@ -3,9 +3,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config default|wide31|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A step = one fused-kernel pass (wab_step) over all B envs of a rank: move, wolves, bushes,
-kill/eat/starve, reward/done, auto-reset and the full observation render, with the inputs
-(actions, pre-generated [W+K, B] int8 on device from torch.randint) resident in HBM.  Each rank
+A step = one fused pass over all B envs of a rank: move, wolves, bushes, kill/eat/starve,
+reward/done, auto-reset and the full observation render, with the inputs (actions,
+pre-generated [W+K, B] int8 on device from torch.randint) resident in HBM.  The line times
+32-step rollout launches (`wab_rollout`; C5 `wab_rollout_features` with the features and the
+segment's returns), the steps' outputs into [32, B] buffers; the per-step launch (`wab_step`,
+the gym `env.step` surface) is timed beside it (`rollout.per_step_launch`; `--rollout 0`
+makes it the line).  Each rank
 owns env ids [rank*B, (rank+1)*B) — independent shards, no collective on the data path
 (weak scaling).  Timing: barrier + synchronize on both sides of exactly K steps, max over
 ranks; value = N*B*K / that time.  Rank 0 prints one JSON line.
