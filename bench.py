@@ -6,8 +6,8 @@
 A step = one fused pass over all B envs of a rank: move, wolves, bushes, kill/eat/starve,
 reward/done, auto-reset and the full observation render, with the inputs (actions,
 pre-generated [W+K, B] int8 on device from torch.randint) resident in HBM.  The line times
-32-step rollout launches (`wab_rollout`; C5 `wab_rollout_features` with the features and the
-segment's returns), the steps' outputs into [32, B] buffers; the per-step launch (`wab_step`,
+64-step rollout launches (`wab_rollout`; C5 `wab_rollout_features` with the features and the
+segment's returns), the steps' outputs into [64, B] buffers; the per-step launch (`wab_step`,
 the gym `env.step` surface) is timed beside it (`rollout.per_step_launch`; `--rollout 0`
 makes it the line).  Each rank
 owns env ids [rank*B, (rank+1)*B) — independent shards, no collective on the data path
@@ -52,8 +52,12 @@ CONFIGS = {
                      "PragmaticObsWrapper features + discounted returns of each %d-step segment "
                      "(episodes crossing a segment end are cut there, R_T = 0), random policy"),
 }
-C5_SEGMENT = 32  # rollout segment length T (actor_critic.py collects one episode, <= 80 steps)
-DEFAULT_ROLLOUT = 32  # steps per wab_rollout launch of the default config's line
+# steps per rollout launch of every config's line, and C5's return segment (actor_critic.py
+# collects one episode per update, <= max_turns = 80 steps).  Measured at B = 65536 on the
+# default config: T = 16 6.55, 32 6.35, 64 6.20, 128 6.11-6.17 us per step (fewer launch
+# boundaries: each costs the launch gap, step 0's state loads and the last step's tail)
+C5_SEGMENT = 64
+DEFAULT_ROLLOUT = 64
 
 
 def committed_traffic(config, batch):
