@@ -58,6 +58,29 @@ CONFIGS = {
 # boundaries: each costs the launch gap, step 0's state loads and the last step's tail)
 C5_SEGMENT = 64
 DEFAULT_ROLLOUT = 64
+# the timed window's floor, whatever --steps asks: at least this many launches of the line's
+# kernel in the captured graph, and graph replays until at least this many seconds are timed
+# (a one-launch window, 0.4 ms, is at the mercy of one launch's jitter)
+MIN_TIMED_LAUNCHES = 32
+MIN_TIMED_SECONDS = 0.2
+
+
+def window_steps(requested, steps_per_launch, min_launches=MIN_TIMED_LAUNCHES):
+    """Steps captured in the timed graph: the requested count in whole launches (at least one),
+    raised to `min_launches` launches."""
+    per = max(1, int(steps_per_launch))
+    k = max(per, int(requested) // per * per)
+    return max(k, min_launches * per)
+
+
+def window_replays(graph_seconds, min_seconds=MIN_TIMED_SECONDS, cap=10000):
+    """Replays of the captured graph that make the timed window at least `min_seconds`, given
+    one replay's measured duration."""
+    import math
+
+    if graph_seconds <= 0:
+        return cap
+    return max(1, min(cap, int(math.ceil(min_seconds / graph_seconds))))
 
 
 def committed_traffic(config, batch):
@@ -166,6 +189,45 @@ def cpu_baseline(opts, stride, seconds, threads, with_features=False):
                       "oracle/wab_oracle.c %s, %d envs x %d steps (%.1f s), 1 thread" % (what, Bc, n, el)}
 
 
+def make_policy(F, n_actions, dev, seed=0):
+    """actor_critic.py's Policy (actor_critic.py:54-97: 449 -> 128 -> 150 -> 128, leaky_relu,
+    clamp(-4, 4), softmax action head and a value head) in stock torch, fp32, random init, and
+    select_action's sampling (:108-125): the features plus U(0, 1)/100 noise, a Categorical draw
+    by inverse CDF over the probabilities (torch.rand only, so the whole step captures in a
+    graph).  act(features [B, F], out [B] int8) writes the sampled actions."""
+    import torch
+    import torch.nn.functional as Fn
+
+    torch.manual_seed(seed)
+
+    class Policy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.affine1 = torch.nn.Linear(F, 128)
+            self.affine2 = torch.nn.Linear(128, 150)
+            self.affine3 = torch.nn.Linear(150, 128)
+            self.action_head = torch.nn.Linear(128, n_actions)
+            self.value_head = torch.nn.Linear(128, 1)
+
+        def forward(self, x):
+            x = Fn.leaky_relu(self.affine1(x))
+            x = Fn.leaky_relu(self.affine2(x))
+            x = Fn.leaky_relu(self.affine3(x))
+            x = torch.clamp(x, -4, 4)
+            return Fn.softmax(self.action_head(x), dim=-1), self.value_head(x)
+
+        @torch.no_grad()
+        def act(self, feats, out):
+            probs, value = self(feats + torch.rand_like(feats) / 100)
+            u = torch.rand((feats.shape[0], 1), device=feats.device)
+            a = (probs.cumsum(-1) < u).sum(-1).clamp_(max=n_actions - 1)
+            out.copy_(a)
+            self.last_value = value
+            return out
+
+    return Policy().to(dev).eval()
+
+
 def probe_device_count():
     """GPUs visible to a fresh process, counted in a child so this (launcher) process never
     touches the GPU runtime before it starts the ranks."""
@@ -239,11 +301,23 @@ def main():
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
                     help="override the config's wolf rows per env (0: the config's own; the wide "
                          "kernel keeps 8 of them in registers)")
+    ap.add_argument("--policy", default="random", choices=["random", "mlp"],
+                    help="c5 only.  random: actions drawn up front (the line's open-loop rollout); "
+                         "mlp: closed loop, each step's actions sampled from actor_critic.py's "
+                         "Policy (449-128-150-128-{5,1}, stock torch, fp32, random init) on the "
+                         "previous step's features, then one wab_step_features launch; graph-captured")
     ap.add_argument("--c5-unfused", action="store_true",
                     help="C5 as wab_step + wab_featurize (obs planes stored) instead of wab_step_features")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.policy == "mlp" and args.config != "c5":
+        raise SystemExit("bench.py: --policy mlp needs --config c5 (the policy reads the features)")
+    if args.rollout < 0:
+        args.rollout = DEFAULT_ROLLOUT if not (args.c5_unfused or args.policy == "mlp") else 0
+    if args.policy == "mlp" and args.rollout > 0:
+        raise SystemExit("bench.py: --policy mlp picks each step's action from that step's features: "
+                         "one launch per step (--rollout 0)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(self_launch(args))
 
@@ -273,8 +347,6 @@ def main():
     opts, stride, slots, desc = CONFIGS[args.config]
     slots = args.wolf_slots or slots
     c5 = args.config == "c5"
-    if args.rollout < 0:
-        args.rollout = DEFAULT_ROLLOUT if not args.c5_unfused else 0
     c5_roll = c5 and args.rollout > 0
     if c5_roll:
         args.rollout = C5_SEGMENT if args.rollout <= 0 else args.rollout
@@ -290,11 +362,16 @@ def main():
     if c5:
         seg = T_roll if c5_roll else C5_SEGMENT
         desc = desc % seg
-        K = max(seg, K // seg * seg)  # whole segments
+        per_launch_steps = seg if c5_roll else 1
         W = max(seg, -(-W // seg) * seg)
+        K = window_steps(K, seg, MIN_TIMED_LAUNCHES if c5_roll else MIN_TIMED_LAUNCHES * seg)
     elif rollout:
-        K = max(args.rollout, K // args.rollout * args.rollout)  # whole segments
+        per_launch_steps = args.rollout
         W = -(-W // args.rollout) * args.rollout
+        K = window_steps(K, args.rollout)
+    else:
+        per_launch_steps = 1
+        K = window_steps(K, 1)
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
@@ -307,7 +384,7 @@ def main():
     if c5:
         T = T_roll if c5_roll else C5_SEGMENT
         F = int(L.wab_feature_dim(h))
-        feats = torch.empty((T, B, F), dtype=torch.float32, device=dev)
+        feats = torch.zeros((T, B, F), dtype=torch.float32, device=dev)
         seg_rew = torch.zeros((T, B), dtype=torch.float32, device=dev)
         seg_done = torch.zeros((T, B), dtype=torch.uint8, device=dev)
         seg_ret = torch.empty((T, B), dtype=torch.float32, device=dev)
@@ -329,8 +406,22 @@ def main():
             rc = L.wab_step(h, a0 + t * B, obs_addr, r0 + 4 * i * B, d0 + i * B, None, s)
             return rc or L.wab_featurize(h, obs_addr, None, f0 + 4 * i * B * F, s)
 
+        policy = None
+        if args.policy == "mlp":
+            policy = make_policy(F, env.n_actions, dev)
+
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
+            if policy is not None:  # closed loop: each step's action from the policy on the last features
+                for t in range(t0, t0 + n):
+                    i = t % T
+                    prev = feats[(i - 1) % T]
+                    policy.act(prev, actions[t])
+                    _lib.check(c5_step(t, i, s), "c5 step")
+                    if i == T - 1:
+                        _lib.check(L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s),
+                                   "wab_discounted_returns_exact")
+                return
             if c5_roll:  # one launch per segment: T fused steps and the segment's returns
                 for t in range(t0, t0 + n, T):
                     _lib.check(L.wab_rollout_features(h, a0 + t * B, T, rseq_addr, r0, d0, f0, 0.99, None, ret0, s),
@@ -400,6 +491,22 @@ def main():
         run(0, W, stream)
         torch.cuda.synchronize(dev)
 
+    def replay_once():
+        if graph is not None:
+            graph.replay()
+        else:
+            run(W, K, stream)
+
+    # calibration (untimed): one replay of the window's K steps sizes the replay count
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record(stream)
+    replay_once()
+    c1.record(stream)
+    torch.cuda.synchronize(dev)
+    reps = window_replays(c0.elapsed_time(c1) * 1e-3)
+    if world > 1:  # every rank times the same number of steps
+        reps = int(max_over_ranks(reps))
+
     c_before = env.counters()  # (synchronises; outside the timed region)
     if world > 1:
         dist.barrier()
@@ -407,28 +514,34 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    if graph is not None:
-        graph.replay()
-    else:
-        run(W, K, stream)
+    for _ in range(reps):
+        replay_once()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
+    wall_rank = time.perf_counter() - t0
+    # each rank's time is its own launch stream's, from the HIP events around the window; the
+    # MAX over ranks is taken afterwards (no barrier inside the window)
+    stream_ms = ev0.elapsed_time(ev1)
+    elapsed_rank = stream_ms * 1e-3
     if world > 1:
         dist.barrier()
-    elapsed_rank = time.perf_counter() - t0
-    stream_ms = ev0.elapsed_time(ev1)
     elapsed = max_over_ranks(elapsed_rank)
+    K_req, K = K, K * reps  # steps in the graph; steps timed
     c_after = env.counters()
     window = {"env_steps": c_after["steps"] - c_before["steps"],
-              "resets": c_after["resets"] - c_before["resets"]}
+              "resets": c_after["resets"] - c_before["resets"],
+              "graph_steps": K_req, "graph_replays": reps,
+              "launches": K // per_launch_steps,
+              "stream_ms": round(stream_ms, 3), "wall_ms": round(wall_rank * 1e3, 3)}
     window["resets_per_env_step"] = round(window["resets"] / max(1, window["env_steps"]), 5)
+    window["floor"] = {"min_launches": MIN_TIMED_LAUNCHES, "min_seconds": MIN_TIMED_SECONDS}
 
     # kernel duration: the HIP events around the timed region on the launch stream give the
     # average per launch (back-to-back graph launches: kernel time plus the launch gap, the
     # figure rocprofv3's average agrees with); events bracketing single launches (below, not
     # timed above) add their own overhead and are reported as a diagnostic only
     kern_ms = stream_ms / K
-    n_k = min(K, 200)
+    n_k = min(K_req, 200)  # (the actions buffer holds W + K_req steps)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_k)]
     s = ctypes.c_void_p(stream.cuda_stream)
     for i in range(n_k):
@@ -474,17 +587,34 @@ def main():
         # measured beside the rollout line; a rollout launch moves the state once per T steps
         # (loaded by its first step, stored by its last), so its algorithmic bytes per env-step
         # are the obs, action, scalars, reward and done plus 2 * 36 / T of state
-        ps_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), min(K, 512))
+        # into a 32-slot ring of [B] obs buffers (step t into slot t % 32, so the stores reach
+        # HBM as the rollout's do) and, as a diagnostic, into one [B] buffer rewritten every step
+        # (which the 256 MB Infinity Cache can hold)
+        NR = 32
+        ring_planes = torch.empty((NR, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+        ring_scal = torch.empty((3, NR, B), dtype=torch.uint8, device=dev)
+        ring_rd = torch.empty((NR, B, 5), dtype=torch.uint8, device=dev)  # reward f32 + done u8
+        ring_obs = [_lib.WabObs(ring_planes[i].data_ptr(), ring_scal[0, i].data_ptr(), ring_scal[1, i].data_ptr(),
+                                ring_scal[2, i].data_ptr()) for i in range(NR)]
+        ring_addr = [ctypes.addressof(o) for o in ring_obs]
+        rr = torch.empty((NR, B), dtype=torch.float32, device=dev)
+        n_ps = min(K_req, 512)
+        ps_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, ring_addr[i % NR], rr[i % NR].data_ptr(),
+                                                   ring_rd[i % NR].data_ptr(), None, s), n_ps)
+        psc_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_ps)
+        del ring_planes
         roll_line = {"steps_per_launch": T_roll, "launch_us": round(kern_ms * T_roll * 1e3, 3),
-                     "per_step_launch": {"api": "wab_step (BatchedWolvesAndBushesEnv.step)",
+                     "per_step_launch": {"api": "wab_step (BatchedWolvesAndBushesEnv.step), obs into a "
+                                                "%d-slot ring of [B] buffers" % NR,
                                          "us_per_step": round(ps_ms * 1e3, 3),
                                          "env_steps_per_s": round(B / (ps_ms * 1e-3), 1),
                                          "alg_bytes_per_env_step": alg,
-                                         "frac": round(alg * B / (ps_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+                                         "frac": round(alg * B / (ps_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                         "one_buffer_us_per_step": round(psc_ms * 1e3, 3)}}
         alg = alg_bytes_per_env_step_rollout(env.W, env.H, T_roll)
         kernel_name = "wab_step_%s, rollout build (%d steps per launch)" % (L.wab_step_kernel(h).decode(), T_roll)
     if c5:
-        n_k = min(K, 512)
+        n_k = min(K_req, 512)
         ret_ms = per_launch(lambda i, s: L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s), 64)
         if fused:
             sf_ms = per_launch(lambda i, s: L.wab_step_features(h, a0 + (W + i) * B, fobs_addr, rew, done,
@@ -497,8 +627,10 @@ def main():
                        "step_features_us": round(sf_ms * 1e3, 3),
                        "returns_us_per_segment": round(ret_ms * 1e3, 3),
                        "returns_frac": round(RETURNS_ALG_BYTES * T * B / (ret_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                       "alg_bytes_per_env_step": sf_alg + RETURNS_ALG_BYTES,
-                       "achieved_GBs_whole_step": round((sf_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)}
+                       "alg_bytes_per_env_step": sf_alg + RETURNS_ALG_BYTES}
+            if not c5_roll and policy is None:
+                # the per-step line: the fused launch's bytes + the scan's, over the timed step
+                c5_line["achieved_GBs_whole_step"] = round((sf_alg + RETURNS_ALG_BYTES) * B / (kern_ms * 1e-3) / 1e9, 1)
             kernel_name = "wab_step_%s + PragmaticObsWrapper features (wab_step_features)" % L.wab_step_kernel(h).decode()
             if c5_roll:
                 # the line's kernel is the rollout launch itself (kern_ms: per step from the
@@ -509,6 +641,21 @@ def main():
                 kernel_name = ("wab_step_%s + PragmaticObsWrapper features + returns, rollout build (%d steps "
                                "per launch, wab_rollout_features)" % (L.wab_step_kernel(h).decode(), T))
             else:
+                if policy is not None:
+                    # closed loop: the timed step is the policy forward + sample + the fused env
+                    # launch (+ the scan every T steps); the env's share from its own launches
+                    def policy_only(i, s):
+                        policy.act(feats[i % T], actions[W + i])
+                        return 0
+                    pol_ms = per_launch(policy_only, n_k)
+                    step_total = kern_ms
+                    c5_line["policy"] = {
+                        "model": "actor_critic.py Policy 449-128-150-128-{%d,1}, fp32 stock torch, "
+                                 "random init; Categorical sample by inverse CDF" % env.n_actions,
+                        "us_per_step": round(step_total * 1e3, 3),
+                        "policy_us": round(pol_ms * 1e3, 3),
+                        "env_us": round(sf_ms * 1e3 + ret_ms * 1e3 / T, 3),
+                        "env_share": round((sf_ms + ret_ms / T) / step_total, 4)}
                 alg, kern_ms = sf_alg, sf_ms
         step_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_k)
         feat_ms = per_launch(lambda i, s: L.wab_featurize(h, obs_addr, None, f0 + 4 * (i % T) * B * F, s), n_k)
@@ -531,7 +678,8 @@ def main():
     achieved_rank = alg * B / (kern_ms * 1e-3) / 1e9
     per_rank = all_gather_objects({
         "rank": rank, "device": str(dev), "pci": pci_id(dev), "env_steps_per_s": round(B * K / elapsed_rank, 1),
-        "ms_per_step": round(elapsed_rank * 1e3 / K, 5), "kernel_us": round(kern_ms * 1e3, 3),
+        "ms_per_step": round(elapsed_rank * 1e3 / K, 5), "stream_ms": round(stream_ms, 3),
+        "wall_ms": round(wall_rank * 1e3, 3), "kernel_us": round(kern_ms * 1e3, 3),
         "achieved_GBs": round(achieved_rank, 1), "frac": round(achieved_rank / HBM_PEAK_GBS, 4),
         "timed_window": window, "overflow": counters["wolf_overflow"] + counters["eaten_overflow"],
         "handoff_timeouts": counters["handoff_timeouts"]})
@@ -549,6 +697,7 @@ def main():
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
+            "steps_requested": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / K, 5),
             "higher_is_better": True,

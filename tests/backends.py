@@ -57,3 +57,32 @@ class GpuBackend:
 
     def state(self):
         return self.env.state()
+
+
+class GpuRolloutBackend:
+    """The product's multi-step path: BatchedWolvesAndBushesEnv.rollout -> wab_rollout (one
+    launch for the whole segment; no terminal observations, the bench's auto-reset path)."""
+
+    wolf_slots = 32
+
+    def __init__(self, opts, base, n, autoreset, stride, seed=SEED):
+        from wab_gym_amd.env import BatchedWolvesAndBushesEnv
+
+        self.env = BatchedWolvesAndBushesEnv(opts, num_envs=n, seed=seed, device="cuda:0",
+                                             env_id_base=base, autoreset=autoreset,
+                                             plane_stride=stride, wolf_slots=self.wolf_slots)
+
+    def reset(self):
+        obs = self.env.reset()
+        return (self.env._obs["planes"].cpu().numpy(), obs[3].cpu().numpy(), obs[4].cpu().numpy(),
+                obs[5].cpu().numpy())
+
+    def rollout(self, actions):
+        import torch
+
+        planes, scal, rew, done = self.env.rollout(torch.as_tensor(np.asarray(actions, np.int64)))
+        s = scal.cpu().numpy()
+        return (planes.cpu().numpy(), s[:, 0], s[:, 1], s[:, 2], rew.cpu().numpy(), done.cpu().numpy())
+
+    def state(self):
+        return self.env.state()

@@ -102,6 +102,51 @@ def replay(name, make, plane_stride=0, check_state=True, max_steps=None):
     return steps
 
 
+def replay_rollout(name, make, plane_stride=0, segments=(1, 7, 64)):
+    """Replay a golden set through a multi-step backend: `make(...)` as for replay(), with
+    reset() as there and rollout(actions [n, B]) -> per step (planes, food_turns, role, status,
+    reward, done) numpy arrays [n, ...].  The set's T steps run as consecutive rollouts of the
+    lengths in `segments` (cycled; state carried across calls), every step compared with the
+    golden obs/reward/done, and the hidden state after every rollout with the golden state of
+    its last step (envs that did not just finish)."""
+    g = load(name)
+    meta = g["meta"]
+    W, H = meta["width"], meta["height"]
+    S = plane_stride or H
+    T = meta["T"]
+    autoreset = meta["protocol"] == "autoreset"
+    steps = 0
+    for e0, base, n in groups(meta["env_ids"]):
+        sl = slice(e0, e0 + n)
+        be = make(meta["options"], base, n, autoreset, plane_stride)
+        planes, food, role, status = be.reset()
+        _check_obs("reset", (planes, food, role, status), g["reset0_bits"][sl],
+                   g["reset0_scalars"][sl], W, H, S, -1, e0)
+        t0, k = 0, 0
+        while t0 < T:
+            L = min(segments[k % len(segments)], T - t0)
+            k += 1
+            planes, food, role, status, reward, done = be.rollout(g["actions"][t0:t0 + L, sl])
+            for i in range(L):
+                t = t0 + i
+                gdone = g["done"][t, sl]
+                _cmp("done", done[i].astype(bool), gdone, t, e0)
+                _cmp("reward", reward[i].astype(np.float32), g["reward"][t, sl].astype(np.float32), t, e0)
+                d = gdone if autoreset else np.zeros(n, bool)
+                bits = np.where(d[:, None], g["rbits"][t, sl], g["bits"][t, sl])
+                sc = np.where(d[:, None], g["rscalars"][t, sl], g["scalars"][t, sl])
+                _check_obs("rollout obs", (planes[i], food[i], role[i], status[i]), bits, sc, W, H, S, t, e0)
+            t = t0 + L - 1
+            st = be.state()
+            nd = ~(g["done"][t, sl].astype(bool) if autoreset else np.zeros(n, bool))
+            _cmp("food(f64)", st["food"][nd].view(np.uint64), g["food"][t, sl][nd].view(np.uint64), t, e0)
+            _cmp("pos", np.stack([st["x"], st["y"]], 1)[nd], g["pos"][t, sl][nd], t, e0)
+            _cmp("n_wolves", st["n_wolves"][nd], g["n_wolves"][t, sl][nd], t, e0)
+            t0 += L
+            steps += n * L
+    return steps
+
+
 def _check_obs(what, obs, bits, scalars, W, H, S, t, e0):
     planes, food, role, status = obs
     want = unpack(bits, W, H)

@@ -28,6 +28,28 @@ def test_gpu_matches_reference_golden(name):
     assert gr.replay(name, GpuBackend) > 0
 
 
+@pytest.mark.parametrize("name", gr.SETS)
+def test_gpu_rollout_matches_reference_golden(name):
+    """Every golden set through env.rollout (wab_rollout: the multi-step launches bench.py
+    times), in consecutive rollouts of 1, 7 and 64 steps with the state carried across them."""
+    from backends import GpuRolloutBackend
+
+    assert gr.replay_rollout(name, GpuRolloutBackend) > 0
+
+
+def test_gpu_rollout_golden_wide_kernel_and_8_slots():
+    """The wide kernel's rollout build (31x31 in 32-byte rows, C3's layout) and the small one
+    with 8 wolf rows (the headline's handle) on the golden sets."""
+    from backends import GpuRolloutBackend
+
+    class Slots8(GpuRolloutBackend):
+        wolf_slots = 8
+
+    assert gr.replay_rollout("wide31", GpuRolloutBackend, plane_stride=32) > 0
+    assert gr.replay_rollout("wolfy", GpuRolloutBackend, plane_stride=16, segments=(64, 5)) > 0  # 16-byte rows: wide kernel
+    assert gr.replay_rollout("default", Slots8) > 0
+
+
 def test_gpu_golden_8_slots_and_padded_stride():
     class Slots8(GpuBackend):
         wolf_slots = 8
@@ -785,14 +807,15 @@ def test_rollout_features_equals_step_features_loop(opts, kw, T, planes):
 
 
 def test_rollout_features_full_size_c5():
-    """C5 at full size (B = 65536, T = 32, the bench's segment): the single rollout launch ==
-    32 fused step launches + the exact returns scan, bit for bit, twice in a row; the returns
-    equal the reference's recursion run in float64 on the host for a sample of envs."""
+    """C5 at full size (B = 65536, T = 64 = bench.py's C5_SEGMENT): the single rollout launch ==
+    64 fused step launches + the exact returns scan, bit for bit, twice in a row; the returns
+    equal the reference's recursion run in float64 on the host for a sample of envs.  (The
+    same launches against the oracle: tests/test_gpu_bench_parity.py.)"""
     import torch
 
     from wab_gym_amd.wrappers import discounted_returns
 
-    B, T = 65536, 32
+    B, T = 65536, 64
     e1, e2 = _env(None, B, validate_actions=False), _env(None, B, validate_actions=False)
     e1.reset()
     e2.reset()
@@ -893,10 +916,12 @@ def test_rollout_tiny_batch(wide):
 
 def test_wide_rollout_full_size_c3():
     """C3 at full size (B = 65536, 31x31 in 32x32 planes, 8 register wolves + HBM rows to 32):
-    two 32-step rollout launches == 64 wab_step launches, bit for bit, past the first mass reset."""
+    two 64-step rollout launches (bench.py's T) == 128 wab_step launches, bit for bit, past the
+    turn-40 and turn-80 mass resets.  (The same launches against the oracle:
+    tests/test_gpu_bench_parity.py.)"""
     import torch
 
-    B, T = 65536, 32
+    B, T = 65536, 64
     kw = dict(validate_actions=False, plane_stride=32, wolf_slots=32)
     opts = {"width": 31, "height": 31}
     e1, e2 = _env(opts, B, **kw), _env(opts, B, **kw)
@@ -950,3 +975,39 @@ def test_rollout_short_segments(wide, T):
             feats, rw, dn, _, _ = _step_features_loop(e4, a, 449, False)
             assert torch.equal(r["features"], feats) and torch.equal(r["reward"], rw), seg
             assert torch.equal(r["returns"], discounted_returns(rw, dn, gamma=0.99, env=e4)), seg
+
+
+def test_env_buffers_after_rollouts():
+    """After env.rollout the env's obs, reward and done are the last step's (as after T step()
+    calls); after rollout_features without planes the scalars/reward/done are, and the env's
+    own planes are reported stale (observation()/render() of them raise) until the next step;
+    PragmaticObsWrapper.rollout leaves the wrapper's features at the last step's."""
+    import torch
+
+    from wab_gym_amd.wrappers import PragmaticObsWrapper
+
+    B, T = 640, 12
+    e1, e2 = _env(None, B, validate_actions=False), _env(None, B, validate_actions=False)
+    e1.reset()
+    e2.reset()
+    a = torch.as_tensor(np.random.RandomState(1).randint(5, size=(T, B)))
+    planes, scal, rew, done = e1.rollout(a)
+    for t in range(T):
+        e2.step(a[t])
+    assert torch.equal(e1._obs["planes"], e2._obs["planes"]) and torch.equal(e1._obs["planes"], planes[-1])
+    assert torch.equal(e1._obs["scalars"], e2._obs["scalars"])
+    assert torch.equal(e1.reward, e2.reward) and torch.equal(e1.done, e2.done)
+    w1, w2 = PragmaticObsWrapper(e1), PragmaticObsWrapper(e2)
+    assert torch.equal(w1.observation(), w2.observation())
+    f, r, d, ret = w1.rollout(a)
+    for t in range(T):
+        w2.step(a[t])
+    assert torch.equal(w1.features, f[-1]) and torch.equal(w1.features, w2.features)
+    assert torch.equal(e1.reward, e2.reward) and torch.equal(e1._obs["scalars"], e2._obs["scalars"])
+    with pytest.raises(RuntimeError):
+        w1.observation()
+    with pytest.raises(RuntimeError):
+        e1.render(scale=1)
+    e1.step(a[0])
+    e2.step(a[0])
+    assert torch.equal(w1.observation(), w2.observation())

@@ -37,3 +37,19 @@ def test_golden_sets_cover_the_dynamics():
         seen["ate"] += int((np.isclose(r, eat) | np.isclose(r, eat - 1) | np.isclose(r, eat + 1)).sum())
         seen["multi_wolf"] += int((g["n_wolves"] >= 2).sum())
     assert all(v > 0 for v in seen.values()), seen
+
+
+class _OracleRollout(OracleBackend):
+    """A multi-step oracle backend for gr.replay_rollout (the harness the GPU rollout replay
+    uses), stepping the oracle once per row of the segment."""
+
+    def rollout(self, actions):
+        import numpy as np
+
+        out = [self.step(a)[:6] for a in actions]
+        return tuple(np.stack([o[k] for o in out]) for k in range(6))
+
+
+@pytest.mark.parametrize("name", ["default", "continue", "wolfy"])
+def test_rollout_replay_harness_on_oracle(name):
+    assert gr.replay_rollout(name, _OracleRollout) > 0

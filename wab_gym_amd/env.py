@@ -88,6 +88,7 @@ class BatchedWolvesAndBushesEnv:
         self._masks = torch.as_tensor(view_masks(opts), device=dev)
         self._zero_mask = torch.zeros((11, 11), **u8)
         self._reset_once = False
+        self._planes_valid = True  # False while the obs planes buffer is stale (planes not stored)
         self.n_actions = n_actions(opts)
         self.action_space = Discrete(self.n_actions)  # wab_env.py:188-191
         W, H = self.W, self.H
@@ -143,8 +144,10 @@ class BatchedWolvesAndBushesEnv:
         """Reset all envs (mask=None) or those with mask[i] true; returns the batched obs."""
         t = self._torch
         m = None
-        if self.validate_actions == "deferred" and self._reset_once:
-            # a deferred out-of-range action must not disappear behind the new episodes
+        if self.validate_actions == "deferred" and self._reset_once and mask is None:
+            # a deferred out-of-range action must not disappear behind the new episodes (this
+            # reads the device counters: a synchronisation, on full resets only; a masked reset
+            # leaves the check to the next counters()/state()/check())
             self._raise_pending(self._read_counters(), None)
         if mask is not None:
             if not self._reset_once:
@@ -157,6 +160,8 @@ class BatchedWolvesAndBushesEnv:
                    "wab_reset")
         self._reset_mask_keepalive = m
         self._reset_once = True
+        if m is None:
+            self._planes_valid = True
         return self._obs_tuple(self._obs)
 
     def _step_actions(self, actions):
@@ -240,6 +245,7 @@ class BatchedWolvesAndBushesEnv:
         _lib.check(_lib.load().wab_step(self._h, a.data_ptr(), ctypes.addressof(self._obs["struct"]),
                                         self.reward.data_ptr(), self.done.data_ptr(), term,
                                         self._stream()), "wab_step")
+        self._planes_valid = True
         info = {}
         if self._term is not None:
             info["terminal_obs"] = self._obs_tuple(self._term)
@@ -258,6 +264,7 @@ class BatchedWolvesAndBushesEnv:
                                                  self.reward.data_ptr(), self.done.data_ptr(),
                                                  features.data_ptr(), self._stream()),
                    "wab_step_features")
+        self._planes_valid = bool(store_planes)
         return features, self.reward, self.done.view(self._torch.bool)
 
     def rollout(self, actions):
@@ -280,7 +287,16 @@ class BatchedWolvesAndBushesEnv:
         _lib.check(_lib.load().wab_rollout(self._h, a.data_ptr(), T, ctypes.addressof(o),
                                            rew.data_ptr(), done.data_ptr(), self._stream()),
                    "wab_rollout")
+        if T > 0:  # the env's buffers show the last step, as after T step() calls
+            self._obs["planes"].copy_(planes[T - 1])
+            self._sync_last_step(scal[:, T - 1], rew[T - 1], done[T - 1])
         return planes, scal.permute(1, 0, 2), rew, done
+
+    def _sync_last_step(self, scal, rew, done):
+        self._obs["scalars"].copy_(scal)
+        self.reward.copy_(rew)
+        self.done.copy_(done)
+        self._planes_valid = True
 
     def rollout_features(self, actions, gamma=0.99, bootstrap=None, returns=True, store_planes=False,
                          features=None):
@@ -328,6 +344,16 @@ class BatchedWolvesAndBushesEnv:
                                           None if bs is None else bs.data_ptr(),
                                           None if ret is None else ret.data_ptr(), self._stream()),
                    "wab_rollout_features")
+        if T > 0:
+            # the env's scalars, reward and done show the last step; its planes too when they
+            # were stored -- otherwise they were never written (rendered on chip only) and the
+            # env's obs planes are stale until the next step()/reset() (observation() and
+            # render() of the env's own buffer then raise)
+            self._sync_last_step(scal[:, T - 1], rew[T - 1], done[T - 1])
+            if planes is not None:
+                self._obs["planes"].copy_(planes[T - 1])
+            else:
+                self._planes_valid = False
         return {"features": features, "scalars": scal.permute(1, 0, 2), "reward": rew, "done": done,
                 "returns": ret, "planes": planes}
 
@@ -346,6 +372,7 @@ class BatchedWolvesAndBushesEnv:
             raise ValueError("out must be a contiguous uint8 tensor of shape %s on %s" % (shape, self.device))
         keep = None
         if obs is None:
+            self._require_planes()
             st = self._obs["struct"]
         else:
             st, keep = self._obs_struct(obs)
@@ -353,6 +380,12 @@ class BatchedWolvesAndBushesEnv:
                                           img.data_ptr(), self._stream()), "wab_render")
         del keep
         return img
+
+    def _require_planes(self):
+        if not self._planes_valid:
+            raise RuntimeError("the env's obs planes were not stored by the last call "
+                               "(step_features/rollout_features with store_planes=False); pass obs= "
+                               "or step()/reset() first")
 
     @property
     def step_kernel(self):

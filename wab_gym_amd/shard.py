@@ -49,20 +49,25 @@ def launch_ranks(cmd, n, env=None, master_port=None, timeout=None):
     codes = [None] * n
     t_end = None if timeout is None else time.monotonic() + timeout
     first_failure = 0
-    while any(c is None for c in codes):
-        for r, p in enumerate(procs):
-            if codes[r] is None:
-                codes[r] = p.poll()
-        failed = [c for c in codes if c not in (None, 0)]
-        late = t_end is not None and time.monotonic() > t_end
-        if failed or late:
-            first_failure = failed[0] if failed else -9
+    try:
+        while any(c is None for c in codes):
             for r, p in enumerate(procs):
                 if codes[r] is None:
+                    codes[r] = p.poll()
+            failed = [c for c in codes if c not in (None, 0)]
+            late = t_end is not None and time.monotonic() > t_end
+            if failed or late:
+                first_failure = failed[0] if failed else -9
+                break
+            time.sleep(0.05)
+    finally:
+        # whatever ends the wait (a failure, the timeout, an exception or KeyboardInterrupt in
+        # this process), no child that may hold the GPU is left running
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                if p.poll() is None:
                     p.kill()
-                    codes[r] = p.wait() or -9
-            break
-        time.sleep(0.05)
+                codes[r] = p.wait()
     th.join(timeout=10)
     return first_failure, "".join(out0), codes
 

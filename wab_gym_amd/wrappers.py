@@ -49,6 +49,7 @@ class PragmaticObsWrapper:
         env = self.env
         t = env._torch
         if obs is None:
+            env._require_planes()
             st = env._obs["struct"]
             keep = None
         else:
@@ -75,6 +76,8 @@ class PragmaticObsWrapper:
         if type(self) is not PragmaticObsWrapper:
             raise NotImplementedError("rollout() fuses PragmaticObsWrapper only")
         r = self.env.rollout_features(actions, gamma=gamma, bootstrap=bootstrap)
+        if r["features"].shape[0] > 0:
+            self.features.copy_(r["features"][-1])  # as after T step() calls
         return r["features"], r["reward"], r["done"].view(self.env._torch.bool), r["returns"]
 
     def step(self, actions):
@@ -115,6 +118,7 @@ class SuperBasicObservationWrapper(PragmaticObsWrapper):
         PragmaticObsWrapper.observation; the view mask is not part of this wrapper)."""
         env = self.env
         if obs is None:
+            env._require_planes()
             st = env._obs["struct"]
             keep = None
         else:
