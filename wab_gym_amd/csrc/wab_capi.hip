@@ -133,7 +133,7 @@ bool small_map(const Params& p) { return p.WHW <= 4; }
 // at exactly 11x11) step with the four-wave small-view kernel (wab_step_small.hip); other
 // views of at most 32 x 32 cells in rows of 16 or 32 bytes without restrict_view step and
 // reset with the wide-view kernel (wab_step_wide.hip, its own bitmap layout: one dword per
-// row).  WAB_STEP_KERNEL=block selects the block kernel for all (A/B measurements).
+// row).
 enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1, KERNEL_WIDE = 2 };
 
 // (W, H >= 3: the strip that scrolls into view, drawn on another wave, never holds the
@@ -502,9 +502,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
   h->n_blocks = (int)((batch + wab::kEnvsPerBlock - 1) / wab::kEnvsPerBlock);
   h->lds_bytes = (size_t)wab::lds_layout(p, slots).total * 4u;
   {
-    const char* k = std::getenv("WAB_STEP_KERNEL");
-    const bool forced_block = k && std::strcmp(k, "block") == 0;
-    h->step_kernel = forced_block ? KERNEL_BLOCK : small_view(p) ? KERNEL_SMALL : wide_view(p) ? KERNEL_WIDE : KERNEL_BLOCK;
+    h->step_kernel = small_view(p) ? KERNEL_SMALL : wide_view(p) ? KERNEL_WIDE : KERNEL_BLOCK;
     h->small_lds_bytes = (size_t)wab::small_layout(p).total * 4u;
     // wab_step_features fuses the featurizer into the small kernel when the table-driven
     // featurizer applies (see featurize): every cell within md of the centre row/column
@@ -513,8 +511,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
       q.features = reinterpret_cast<float*>(16);  // (layout only)
       h->small_feat_lds_bytes = (size_t)wab::small_layout(q).total * 4u;
     }
-    const char* g = std::getenv("WAB_SMALL_GENERIC");  // A/B: the runtime-geometry build
-    h->small_g11 = geometry_11(p) && !(g && std::atoi(g));
+    h->small_g11 = geometry_11(p);
   }
   if (h->lds_bytes > 160u * 1024u) {
     delete h;
@@ -589,26 +586,7 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
   if (h->step_kernel == KERNEL_WIDE) {
-    // WAB_WIDE_LDS_KB (experiments): reserve more LDS per workgroup than needed, which caps
-    // the workgroups a CU can hold and so evens out their distribution over the CUs
     h->wide_lds_bytes = (size_t)wab::wide_layout(p).total * 4u;
-    h->p.obs_nt = 0;  // plain stores measured faster than non-temporal for this pattern
-    if (const char* nt = std::getenv("WAB_OBS_NT")) h->p.obs_nt = std::atoi(nt);
-    {
-      int cus = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
-      // off by default: measured neutral once W0 writes the wolf planes early (46.9 vs 47.3 us)
-      h->p.age_cus = 0;
-      h->p.age_shift = 0;
-      if (const char* a = std::getenv("WAB_AGE_PRIO")) {  // experiments: k > 0: priority = age >> (k - 1)
-        if (std::atoi(a) > 0) {
-          h->p.age_cus = cus;
-          h->p.age_shift = std::atoi(a) - 1;
-        }
-      }
-    }
-    if (const char* kb = std::getenv("WAB_WIDE_LDS_KB"))
-      h->wide_lds_bytes = std::max(h->wide_lds_bytes, (size_t)std::atoi(kb) * 1024u);
     for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots),
                     reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots>)})
       if (e == hipSuccess)
@@ -692,8 +670,7 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
   if (int rc = check_obs(obs_seq, "wab_rollout")) return rc;
   const int64_t B = h->p.B;
   const size_t OB = (size_t)h->p.OB;
-  const char* wr = std::getenv("WAB_WIDE_ROLLOUT");  // A/B: 0 = T wab_step launches on the wide kernel
-  const bool wide_roll = h->step_kernel == KERNEL_WIDE && !(wr && std::atoi(wr) == 0);
+  const bool wide_roll = h->step_kernel == KERNEL_WIDE;
   if (T > 0 && (h->step_kernel == KERNEL_SMALL || wide_roll) && h->reset_done && actions && reward && done &&
       ((size_t)B * OB) % 16u == 0) {  // (every step's planes 16-byte aligned)
     // one launch: each workgroup runs its 64 envs through the T steps (Params::n_steps)

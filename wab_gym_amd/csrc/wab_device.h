@@ -162,19 +162,6 @@ __device__ __forceinline__ void bush_thr_pads(uint64_t* thr, int n) {
   thr[n + 1] = ~0ull;
 }
 
-// Workgroups are dispatched round-robin over the CUs, so blockIdx / (number of CUs) is a
-// workgroup's age rank among those sharing its CU.  The SIMD arbiter favours older waves at
-// equal priority; the youngest workgroups then start their stores last and end the launch
-// alone.  Raising the priority of the younger ones (age 0..3 -> s_setprio 0..3) evens it out.
-__device__ __forceinline__ void setprio_age(const Params& p) {
-  if (p.age_cus <= 0) { __builtin_amdgcn_s_setprio(0); return; }
-  const uint32_t age = min(3u, (blockIdx.x / (uint32_t)p.age_cus) >> p.age_shift);
-  if (age >= 3u) __builtin_amdgcn_s_setprio(3);
-  else if (age == 2u) __builtin_amdgcn_s_setprio(2);
-  else if (age == 1u) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
-}
-
 // packed-tile add: both int16 halves wrap independently (v_pk_add_u16)
 typedef unsigned short wab_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t xy_add(uint32_t a, uint32_t b) {

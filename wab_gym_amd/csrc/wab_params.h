@@ -83,9 +83,6 @@ struct Params {
   int32_t start_role, start_food_random, start_role_random;
   int32_t max_turns, turns_empty;
   int32_t lookout_only, restrict_view, wolves_on, wolves_can_move, god_mode, autoreset;
-  int32_t obs_nt;           // wide kernel: obs stores non-temporal (1) or plain (0)
-  int32_t age_shift;        // priority = age >> age_shift
-  int32_t age_cus;          // > 0: issue priority by workgroup age on its CU (blockIdx / age_cus), 0: off
   uint32_t mask_rows[2][11];  // restrict_view: 11-bit row masks per role (bit j <=> mask[i][j])
   uint32_t small_masks[3][4]; // W*H <= 128: column 0, column H-1, valid-bit masks of the bitmap
   uint32_t view121[2][4];     // restrict_view at 11x11: the row masks as one 121-bit plane mask
@@ -167,7 +164,6 @@ struct SmallLayout {
   uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
   uint32_t rcode;       // wab_rollout_features with returns: [n_steps][64] reward codes (bytes)
-  uint32_t fbits2;      // multi-step fused features: the odd steps' feature bits (rows stored a step later)
 };
 
 __host__ __device__ inline SmallLayout small_layout(const Params& p) {
@@ -204,8 +200,6 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
     L.fzero = o - L.fbits;
     L.scal = o; o += 64u;
   }
-  L.fbits2 = o;
-  if (p.features && p.n_steps > 1) o += lds_align4(((64u * (uint32_t)(16 * (p.W / 2 + p.H / 2 + 2) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121) + 31u) >> 5) + 4u);
   L.rcode = o;
   if (p.returns) o += 16u * (uint32_t)p.n_steps;  // one byte per env and step
   L.total = o;

@@ -261,8 +261,8 @@ struct Lds {
   uint64_t* gap;    // [n_gap + 1] spawn-set gap table (W3; read on a hit only)
   uint32_t* stream; // 64 envs x OB bits: bit k = byte k of the group's obs chunk
   uint32_t* cval;   // [64] generated berries of the ostrich's tile (W1), then flag[0] = 1
-  uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done, [2] S rendered (W2,
-                    // early obs stores); zeroed by W0 before B_init
+  uint32_t* flag;   // [0] tile values ready (W1), [1] W1's reset draws done; zeroed by W0
+                    // before B_init
   uint4* wolfp;     // [64] wolf grid of S (W2, P0)
   uint32_t* kill;   // [64] (W2, P0)
   uint4* bushp;     // [64] bush grid of S without the entering strip (W0, P0)
@@ -307,33 +307,17 @@ __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u
 // (Measured and reverted: the key-only part of the new episodes on W0 after its own P1 work
 // instead of on W3 before its wait for W1: 9.05 -> 9.57 us.)
 // After B1 the new episodes (W3) are the longest chain: W3 is raised to the top issue
-// priority there and W0 lowered (A/B at B = 65536: 10.05 -> 10.02 us; -DWAB_P1_PRIO=0 off).
-// Measured and dropped: priority by workgroup age for the helper waves (+0.09 us), two or
-// four groups per workgroup (one barrier for all: 11.2 / 12.1 us), the spawn sets' gap
-// thresholds evaluated without a table (binary powering from 16 doubles in the kernel
+// priority there and W0 lowered (A/B at B = 65536: 10.05 -> 10.02 us); in multi-step launches
+// W3 goes back to 0 when a step starts.  W1 runs its reset draws (which W3 waits for) at issue
+// priority 2 in multi-step launches (6.41 -> 6.33 us per step; per-step launches: 9.16-9.19 vs
+// 9.13 us without).  Measured and dropped: priority by workgroup age for the helper waves
+// (+0.09 us), two or four groups per workgroup (one barrier for all: 11.2 / 12.1 us), the spawn
+// sets' gap thresholds evaluated without a table (binary powering from 16 doubles in the kernel
 // arguments: 11.1 us, more SGPR spills; from device memory: 14.0 us).
-#ifndef WAB_P1_PRIO
-#define WAB_P1_PRIO 1
-#endif
-// issue priorities in multi-step launches (A/B): 0 none, 1 as a single step with W3 back at 0
-// when a step starts, 2 as a single step
-#ifndef WAB_ROLL_PRIO
-#define WAB_ROLL_PRIO 1
-#endif
-#define WAB_PRIO(ROLL, V)                                             \
-  do {                                                                \
-    if (!(ROLL) || WAB_ROLL_PRIO != 0) __builtin_amdgcn_s_setprio(V); \
-  } while (0)
-
-#ifndef WAB_W1_RESET_PRIO  // multi-step launches only (per-step: 9.16-9.19 vs 9.13 us at 2)
-#define WAB_W1_RESET_PRIO 2
-#endif
+constexpr int kW1ResetPrio = 2;
 // the entering strip's cells are drawn in two parts, [0, kStripW1) on W1 after the tile value
-// and the rest on W3 after the spawn set (A/B: -DWAB_STRIP_W1=k)
-#ifndef WAB_STRIP_W1
-#define WAB_STRIP_W1 8
-#endif
-constexpr int kStripW1 = WAB_STRIP_W1;
+// and the rest on W3 after the spawn set
+constexpr int kStripW1 = 8;
 __device__ __forceinline__ M128 strip_of(const Params& p, const Lds& s, int lane, int dir) {
   return strip_cells(p, dir, s.strip[lane] | s.strip[64 + lane]);
 }
@@ -384,81 +368,15 @@ __device__ __forceinline__ void render_s(const Params& p, const Lds& s, int lane
   stream_set_ostrich(p, s.stream, ebit, role);
 }
 
-// Early obs stores (plain steps of full groups: no terminal obs, no fused features): the
-// group's obs chunk as 16-byte units (one 16-bit stream unit each), split by whether a unit
-// touches a done env.  Those that do not are final once S is rendered: W0, W1 and W2 store
-// them right after B1 (each wave-instruction 64 consecutive units, 1 KiB) while W3 builds the
-// new episodes; the rest go out after B2.  Every unit is stored exactly once.
-// Measured slower (10.34 -> 12.02 us at B = 65536: the stores of all groups then share the
-// HBM while W0-W2 still have to reach B2), so off unless built with -DWAB_EARLY_OBS=1.
-#ifndef WAB_EARLY_OBS
-#define WAB_EARLY_OBS 0
-#endif
-__device__ __forceinline__ bool early_obs(const Params& p) {
-  return WAB_EARLY_OBS && p.features == nullptr && p.t_planes == nullptr && (int64_t)blockIdx.x * 64 + 64 <= p.B;
-}
+// (Measured and reverted: the obs units that touch no done env stored right after B1 by W0-W2
+// while W3 builds the new episodes: 10.34 -> 12.02 us at B = 65536, the stores of all groups
+// then share the HBM while W0-W2 still have to reach B2.)
 
-__device__ __forceinline__ void store_unit(uint8_t* out, const uint32_t* stream, uint32_t u) {
-  const uint32_t v = reinterpret_cast<const uint16_t*>(stream)[u];
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 q;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) q[k] = (((v >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-  __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
-}
-
-// units [64 k + lane] for k = first, first + stride, ... whose 128-byte line (absolute
-// address) holds a byte of a done env iff `touching` (WAB_EARLY_LINES=1; else the unit's own
-// 16 bytes decide).  A line is then written in one phase: a line written in parts at two
-// times is a partial-line write to HBM.
-#ifndef WAB_EARLY_LINES
-#define WAB_EARLY_LINES 1
-#endif
-__device__ __forceinline__ void store_units(const Params& p, const uint32_t* stream, unsigned long long jm,
-                                            bool touching, int first, int stride, int lane) {
-  const uint32_t OB = (uint32_t)p.OB, full = (64u * OB) >> 4;
-  uint8_t* out = p.planes + (size_t)blockIdx.x * 64u * OB;
-  const uint32_t mis = (uint32_t)reinterpret_cast<uintptr_t>(out) & 127u;  // group start within its line
-  for (uint32_t u = 64u * (uint32_t)first + (uint32_t)lane; u < full; u += 64u * (uint32_t)stride) {
-    uint32_t b0 = 16u * u, b1 = 16u * u + 15u;
-    if (WAB_EARLY_LINES) {  // the line's bytes within the group
-      const uint32_t l0 = (b0 + mis) & ~127u;
-      b0 = l0 > mis ? l0 - mis : 0u;
-      b1 = min(l0 + 127u - mis, 64u * OB - 1u);
-    }
-    const uint32_t e0 = b0 / OB, e1 = b1 / OB;  // (a line may span more than two envs when OB < 128)
-    const bool t = ((jm >> e0) & ((2ull << (e1 - e0)) - 1ull)) != 0ull;
-    if (t == touching) store_unit(out, stream, u);
-  }
-}
-
-// multi-step launches: the previous step's obs stored by W0, W2 and W3 (1; 8 units per thread)
-// or by W0 and W2 (0; 12 units per thread) in their slack before B2 (A/B)
-#ifndef WAB_ROLL_STORE_W3
-#define WAB_ROLL_STORE_W3 0
-#endif
-// multi-step launches: each step's feature rows stored during the next step by W0 and W2 in
-// their slack before B2 (1; double-buffered feature bits), or by all threads at the step's end (0)
-#ifndef WAB_ROLL_FEAT_DEFER
-#define WAB_ROLL_FEAT_DEFER 0
-#endif
-// multi-step launches: feature rows non-temporal (1) or plain (0) (A/B)
-#ifndef WAB_ROLL_FEAT_NT
-#define WAB_ROLL_FEAT_NT 1
-#endif
-#ifndef WAB_ROLL_STORE_BATCH  // multi-step launches: obs units per read/clear/store batch (A/B)
-#define WAB_ROLL_STORE_BATCH 12
-#endif
-#ifndef WAB_ROLL_ALIGN  // multi-step launches: obs store instructions on absolute line boundaries (A/B)
-#define WAB_ROLL_ALIGN 0
-#endif
-// multi-step launches: obs stores non-temporal (1) or plain (0) (A/B)
-#ifndef WAB_ROLL_NT
-#define WAB_ROLL_NT 1
-#endif
 // Multi-step launches (wab_rollout): NT threads (index idx) store NK units each (u = idx + NT
-// * k) of a finished step's stream into `planes` (that step's slice), clearing each unit after
-// its read so the stream can be rendered into again
+// * k) of a finished step's stream into `planes` (that step's slice), non-temporal, clearing
+// each unit after its read so the stream can be rendered into again.  (Measured and not
+// adopted: the store instructions aligned to absolute 128-byte lines, plain stores, the units
+// in smaller read/clear/store batches; the obs stores split over W0, W2 and W3.)
 template <int NT, int NK>
 __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes, uint32_t* stream, int idx) {
   const int64_t g0 = (int64_t)blockIdx.x * 64;
@@ -466,59 +384,34 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
   const uint32_t full = ((uint32_t)min((int64_t)64, p.B - g0) * OB) >> 4;
   uint8_t* out = planes + (size_t)g0 * OB;
   uint16_t* s16 = reinterpret_cast<uint16_t*>(stream);
-  // WAB_ROLL_ALIGN: units shifted by the group's offset within its first 128-byte line (OB odd:
-  // every other group starts mid-line), so that each 64-unit store instruction covers whole
-  // absolute lines; NT * NK - 7 still covers every unit (<= 1532 for odd OB <= 383)
-  const int sh = WAB_ROLL_ALIGN ? (int)((reinterpret_cast<uintptr_t>(out) & 127u) >> 4) : 0;
-  // in batches of KB units (all read, then cleared, then expanded and stored): fewer live
-  // registers than one batch of NK (WAB_ROLL_STORE_BATCH)
-  constexpr int KB = WAB_ROLL_STORE_BATCH < NK ? WAB_ROLL_STORE_BATCH : NK;
+  uint32_t v[NK];
 #pragma unroll
-  for (int k0 = 0; k0 < NK; k0 += KB) {
-    uint32_t v[KB];
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)(idx + NT * k);
+    v[k] = u < full ? (uint32_t)s16[u] : 0u;
+  }
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const int u = idx + NT * (k0 + k) - sh;
-      v[k] = k0 + k < NK && u >= 0 && (uint32_t)u < full ? (uint32_t)s16[u] : 0u;
-    }
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)(idx + NT * k);
+    if (u < full) s16[u] = 0;
+  }
+  if (!planes) return;  // (wab_rollout_features without planes: the stream is only cleared)
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const int u = idx + NT * (k0 + k) - sh;
-      if (k0 + k < NK && u >= 0 && (uint32_t)u < full) s16[u] = 0;
-    }
-    if (!planes) continue;  // (wab_rollout_features without planes: the stream is only cleared)
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)(idx + NT * k);
+    if (u >= full) continue;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 q;
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const int u = idx + NT * (k0 + k) - sh;
-      if (k0 + k >= NK || u < 0 || (uint32_t)u >= full) continue;
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 q;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-      if (WAB_ROLL_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
-      else reinterpret_cast<u32x4*>(out)[u] = q;
-    }
+    for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
   }
 }
 
-// WAB_ROLL_FEAT_DEFER: the previous step's feature rows (its bits in the other buffer) by the
-// 128 threads of W0 and W2
-__device__ __forceinline__ void roll_feature_rows(const Params& p, const SmallLayout& L, const uint32_t* lds, int t,
-                                                  int idx) {
-  const uint32_t F = (uint32_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
-  const int64_t g0 = (int64_t)blockIdx.x * 64;
-  const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
-  const uint32_t* ob = lds + (((t - 1) & 1) ? L.fbits2 : L.fbits);
-  store_feature_bits<WAB_ROLL_FEAT_NT>(ob, p.features - (int64_t)p.B * F + (size_t)g0 * F, n_active * F, idx, 128);
-}
-
-// WAB_ROLL_STORE (A/B of the multi-step launch's obs stores): 0 every thread at the step's end
-// (one stream), 1 step t's by every thread half at the start and half at the end of step t + 1,
-// 2 step t's by W0 and W2 in their slack before B2 of step t + 1 (W1 and W3 never store)
-#ifndef WAB_ROLL_STORE
-#define WAB_ROLL_STORE 2
-#endif
-#ifndef WAB_ROLL_FLOOR  // diagnostic: skip every step's work, keep its obs stores
+// Multi-step launches store step t's obs during step t + 1 (streams alternate), by W0 and W2 in
+// their slack before B2 (W1 and W3 never store).  Diagnostic build -DWAB_ROLL_FLOOR=1: every
+// step's work skipped, its obs stores kept (the store pattern's own floor; results wrong by design)
+#ifndef WAB_ROLL_FLOOR
 #define WAB_ROLL_FLOOR 0
 #endif
 
@@ -534,7 +427,7 @@ struct CarryHdr {
   uint4 hdr;  // the env's header at the start of the next step, as far as this wave uses it
 };
 struct CarryW0 {
-  uint8_t* prev_planes;   // the previous step's obs slice and stream (WAB_ROLL_STORE 2), or null
+  uint8_t* prev_planes;   // the previous step's obs slice and stream, or null
   uint32_t* prev_stream;
   uint4 hdr;
   double food;
@@ -673,12 +566,6 @@ __device__ __forceinline__ void new_episode_b(const Params& p, const Lds& s, int
   if (p.WHW > 3) p.bushmap[3 * p.B + g] = m_word<3>(nbm);
 }
 
-// multi-step launches: the view-mask zero lines stored early in each step (1) or with the rest
-// of the rows (0) (A/B)
-#ifndef WAB_ROLL_EARLY_VIEWS
-#define WAB_ROLL_EARLY_VIEWS 0
-#endif
-
 // --------------------------------------------------------------------------- fused features: early lines
 // The view-mask blocks of the feature rows are all zeros without restrict_view, known before
 // the step has computed anything: the whole 128-byte lines inside them (wab_feat.h) are stored
@@ -792,7 +679,6 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   if (lane == 0 && init) {
     s.flag[0] = 0u;
     s.flag[1] = 0u;
-    s.flag[2] = 0u;
   }
   if (init) lds_barrier();  // B_init: the hand-off flags are clear
   int ne = (int)misc_ne(h.hdr.z), ndep = (int)misc_ndep(h.hdr.z);
@@ -891,7 +777,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
   SMALL_STAMP(3);
   lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
-  if constexpr (WAB_P1_PRIO) WAB_PRIO(ROLL, 1);
+  __builtin_amdgcn_s_setprio(1);
 
   // status (starve overrides kill), reward/done (:328-340), scalars, bushes and food
   const bool killed = s.kill[lane] != 0u;
@@ -936,15 +822,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   count_steps(p);
   const unsigned long long jm = __ballot(job);
   if (lane == 0 && jm) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)__popcll(jm));  // (no-return: a load here would wait for the stores)
-  if (early_obs(p)) {
-    lds_await(p, &s.flag[2]);  // S rendered (W2)
-    store_units(p, s.stream, jm, false, 0, 3, lane);
-  }
-  if (ROLL && carry->prev_stream) {
-    if (WAB_ROLL_STORE_W3) store_units_nt<192, 8>(p, carry->prev_planes, carry->prev_stream, lane);
-    else store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
-  }
-  if (ROLL && WAB_ROLL_FEAT_DEFER && p.features && t > 0) roll_feature_rows(p, L, lds, t, lane);
+  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
   SMALL_STAMP(4);
   lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
   if (p.t_planes) {
@@ -1019,7 +897,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(10);
-  WAB_PRIO(ROLL, 2);  // the tile value is on the bushes wave's path
+  __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
   HeadRaw hr;
   if (ROLL && t > 0) {  // (multi-step launch: the thresholds are in LDS since step 0)
     hr.hdr = carry->hdr;
@@ -1050,8 +928,8 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   s.cval[lane] =
       (uint32_t)bush_value_fast(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1), p.bush_power);
   lds_publish(s.flag);  // every lane: each orders its own cval entry
-  WAB_PRIO(ROLL, 0);
-  if (p.features && !p.restrict_view && (!ROLL || WAB_ROLL_EARLY_VIEWS))  // rows 0..31 (step_features)
+  __builtin_amdgcn_s_setprio(0);
+  if (p.features && !p.restrict_view && !ROLL)  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
   SMALL_STAMP(11);
   s.strip[lane] = strip_draws(p, h, b0, b1, 0, kStripW1);  // generate_bushes (:613-629): the entering strip
@@ -1067,7 +945,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   if (jm) {
     // (W3 waits for these draws before it builds the new episodes: W1 at issue priority 2
     // while it makes them, multi-step launches: 6.41 -> 6.33 us per step, profiles/r03_ab2/)
-    if (ROLL && WAB_W1_RESET_PRIO) __builtin_amdgcn_s_setprio(WAB_W1_RESET_PRIO);
+    if (ROLL) __builtin_amdgcn_s_setprio(kW1ResetPrio);
     if (job) {
       const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
       const int j = __popcll(jm & ((1ull << lane) - 1ull));
@@ -1075,12 +953,9 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     }
     reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm);
     lds_publish(&s.flag[1]);
-    if (ROLL && WAB_W1_RESET_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (ROLL) __builtin_amdgcn_s_setprio(0);
   }
-  if (early_obs(p)) {  // S was rendered by W2
-    lds_await(p, &s.flag[2]);
-    store_units(p, s.stream, jm, false, 1, 3, lane);
-  } else if (h.active && (!job || p.t_planes)) {
+  if (h.active && (!job || p.t_planes)) {
     // S of the continuing envs (and of the done ones when their terminal obs is asked for);
     // needed only at B2, so after the reset draws W3 waits for
     render_s(p, s, lane, info, h.dir);
@@ -1092,7 +967,6 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   if (ROLL && lane == 0) {  // every hand-off of this step is done: clear the flags for the next
     s.flag[0] = 0u;
     s.flag[1] = 0u;
-    s.flag[2] = 0u;
   }
   if (ROLL && !last) {
     const uint32_t status = info_starved(info) ? 1u : killed ? 2u : misc_status(h.hdr.z);
@@ -1218,11 +1092,6 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   const uint32_t info = s.info[lane];
   const bool starved = info_starved(info);
   const bool job = active && p.autoreset && env_done(p, h, starved, kill);
-  const bool early = early_obs(p);
-  if (early) {  // S of the continuing envs, for the early obs stores
-    if (active && !job) render_s(p, s, lane, info, h.dir);
-    lds_publish(&s.flag[2]);
-  }
 
   // spawn_wolves (:325-326): new wolves into free slots (outside the view, not in S)
   unsigned long long wolf_of = 0;
@@ -1258,12 +1127,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   }
   if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
   const unsigned long long jm = __ballot(job);
-  if (early) store_units(p, s.stream, jm, false, 2, 3, lane);
-  if (ROLL && carry->prev_stream) {
-    if (WAB_ROLL_STORE_W3) store_units_nt<192, 8>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
-    else store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
-  }
-  if (ROLL && WAB_ROLL_FEAT_DEFER && p.features && t > 0) roll_feature_rows(p, L, lds, t, 64 + lane);
+  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
   SMALL_STAMP(19);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -1299,12 +1163,11 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
 // --------------------------------------------------------------------------- W3: ring
 template <int SLOTS, int G, bool ROLL = false>
 __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const SmallLayout& L, uint32_t* lds, int lane,
-                                                        CarryHdr* carry = nullptr, int t = 0, bool last = true,
-                                                        uint8_t* prev_planes = nullptr, uint32_t* prev_stream = nullptr) {
+                                                        CarryHdr* carry = nullptr, int t = 0, bool last = true) {
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
-  if (ROLL && WAB_ROLL_PRIO == 1) __builtin_amdgcn_s_setprio(0);  // (raised after B1 of the last step)
+  if (ROLL) __builtin_amdgcn_s_setprio(0);  // (raised after B1 of the last step)
   HeadRaw hr;
   if (ROLL && t > 0) {  // (multi-step launch: the tables are in LDS since step 0)
     hr.hdr = carry->hdr;
@@ -1338,7 +1201,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   }
   if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned;
                      // multi-step launches: the tables once, the bits every step)
-    uint4* z = reinterpret_cast<uint4*>(lds + (ROLL && WAB_ROLL_FEAT_DEFER && (t & 1) ? L.fbits2 : L.fbits));
+    uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
     const uint32_t nz = ROLL && t > 0 ? L.ftab - L.fbits : L.fzero;
     for (uint32_t i = lane; i < nz / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
@@ -1347,7 +1210,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   if (p.features) {
     if (!ROLL || t == 0)
       feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
-    if (!p.restrict_view && (!ROLL || WAB_ROLL_EARLY_VIEWS))  // rows 32..63 (step_features)
+    if (!p.restrict_view && !ROLL)  // rows 32..63 (step_features)
       early_view_zeros(p, 32u, (uint32_t)max((int64_t)0, min((int64_t)32, p.B - (int64_t)blockIdx.x * 64 - 32)), lane);
   }
   const uint64_t ek = mix64(h.kenv ^ (uint64_t)h.hdr.w);
@@ -1360,7 +1223,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   s.strip[64 + lane] = strip_draws(p, h, b0, b1, kStripW1, 1 << 30);  // the entering strip, part 2
   SMALL_STAMP(23);
   lds_barrier();  // B1
-  if constexpr (WAB_P1_PRIO) WAB_PRIO(ROLL, 3);
+  __builtin_amdgcn_s_setprio(3);
   // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
   // (unless the terminal obs is asked for: W0 after B2) the new episodes themselves
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(s.info[lane]), s.kill[lane] != 0u);
@@ -1389,8 +1252,6 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
       if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     }
   }
-  if (ROLL && WAB_ROLL_STORE_W3 && prev_stream)  // the third share of the last step's obs
-    store_units_nt<192, 8>(p, prev_planes, prev_stream, 128 + lane);
   SMALL_STAMP(25);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
@@ -1406,9 +1267,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
 // --------------------------------------------------------------------------- obs stores
 // expand the 64-env bit-stream and store it with 16-byte stores, all 256 threads
 // Multi-step launches: units [K0, K1) of the six per thread of a finished step's stream (p its
-// step's slice), each cleared after its read so the stream can be rendered into again (steps
-// alternate between two streams, and step t's obs go out during step t + 1, half at its start
-// and half at its end, so that the obs stores do not all fall between two steps).  No
+// step's slice), each cleared after its read (the last step's obs, stored at its end).  No
 // partial tail: a multi-step launch needs B * OB % 16 == 0 (wab_rollout).
 template <int K0, int K1>
 __device__ __forceinline__ void store_units_of(const Params& p, uint32_t* stream, int tid) {
@@ -1436,8 +1295,7 @@ __device__ __forceinline__ void store_units_of(const Params& p, uint32_t* stream
     u32x4 q;
 #pragma unroll
     for (int b = 0; b < 4; ++b) q[b] = (((v[k - K0] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    if (WAB_ROLL_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
-    else reinterpret_cast<u32x4*>(out)[u] = q;
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
   }
 }
 
@@ -1500,7 +1358,7 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
   const uint32_t* stream = lds + L.stream;
-  uint32_t* ob = lds + (ROLL && WAB_ROLL_FEAT_DEFER && (t & 1) ? L.fbits2 : L.fbits);
+  uint32_t* ob = lds + L.fbits;
   if ((uint32_t)lane < n_active && wave < 3) {
     const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, at = (uint32_t)lane * F;
     if (wave <= 1) {  // W0 wolves, W1 bushes
@@ -1524,12 +1382,12 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   };
   stamp(36);  // the feature bits emitted
 #endif
-  // (WAB_ROLL_FEAT_DEFER: the rows of a step but the last are stored during the next step by W0
-  // and W2 in their slack before B2, roll_feature_rows; the step's end barrier orders the bits)
-  if (ROLL && WAB_ROLL_FEAT_DEFER && t != p.n_steps - 1) return;
+  // (Measured and not adopted in multi-step launches: the rows of step t stored during step t + 1
+  // by W0 and W2 in their slack, from double-buffered feature bits; the view-mask zero lines
+  // stored early in each step.)  Multi-step launches store the rows non-temporal.
   lds_barrier();
-  constexpr bool NT = ROLL && WAB_ROLL_FEAT_NT;
-  if (p.restrict_view || (ROLL && !WAB_ROLL_EARLY_VIEWS)) store_feature_bits<NT>(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
+  constexpr bool NT = ROLL;
+  if (p.restrict_view || ROLL) store_feature_bits<NT>(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
   else store_rows_skip_views<NT>(ob, p.features + (size_t)g0 * F, n_active * F, F, (int)threadIdx.x, 256);
 #ifdef WAB_STAMPS
   stamp(37);  // wave 0's row stores issued
@@ -1571,21 +1429,6 @@ __device__ __forceinline__ void step_slice(Params& p, int t) {
   p.reward += o;
   p.done += o;
   if (p.features) p.features += o * pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
-}
-
-// Multi-step launches (A/B, WAB_ROLL_STAGGER_NS > 0): the four workgroups that share a CU
-// (blockIdx 256 apart) start their first step k * STAGGER ns apart, k = blockIdx >> 8 & 3, so
-// that their store phases do not coincide (they otherwise stay in phase: they share one drain)
-#ifndef WAB_ROLL_STAGGER_NS
-#define WAB_ROLL_STAGGER_NS 0
-#endif
-__device__ __forceinline__ void roll_stagger() {
-  if (WAB_ROLL_STAGGER_NS > 0) {
-    const uint64_t k = (blockIdx.x >> 8) & 3u;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    const uint64_t until = t0 + k * (uint64_t)(WAB_ROLL_STAGGER_NS / 10);
-    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
-  }
 }
 
 template <int SLOTS, int G, bool FEAT, bool ROLL>
@@ -1630,50 +1473,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     }
     const Params p = wave_params<G, FEAT>(p0);
     const SmallLayout L = small_layout(p);
-    if (!FEAT && early_obs(p)) {  // the units that touch a done env (the rest went out after B1)
-      if (jm) store_units(p, lds + L.stream, jm, true, wave, 4, lane);
-    } else if (!FEAT || p.planes) {
-      store_obs(p, lds + L.stream, threadIdx.x);
-    }
+    (void)jm;
+    if (!FEAT || p.planes) store_obs(p, lds + L.stream, threadIdx.x);
     if constexpr (FEAT) step_features(p, L, lds, wave, lane);
   } else {
     // wab_rollout: n_steps steps of this group, one after the other (the envs of a workgroup
     // depend on nothing outside it), each wave's state carried in registers from step to step
     // (see CarryW0): one barrier closes a step (its LDS is reused by the next)
     const int T = p0.n_steps;
-    roll_stagger();
     {  // the second stream starts clear (the first is cleared by W0 in step 0)
       const SmallLayout L = small_layout(p0);
       uint4* z = reinterpret_cast<uint4*>(lds + L.stream2);
       for (uint32_t i = threadIdx.x; i < L.stream_words / 4u; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
     }
-    // one step of wave W's part; step t renders into stream t & 1 while step t - 1's obs go out
-    // (WAB_ROLL_STORE 1, 2; 0: one stream, stored at the step's end)
+    // one step of wave W's part; step t renders into stream t & 1 while W0 and W2 store step
+    // t - 1's obs from the other one; the last step's obs go out at its end, by every thread
 #define WAB_ROLL_STEP(...)                                                                   \
     for (int t = 0; t < T; ++t) {                                                            \
       Params p = wave_params<G, FEAT>(p0);                                                   \
       step_slice(p, t);                                                                      \
       const SmallLayout L0 = small_layout(p);                                                \
       SmallLayout L = L0;                                                                    \
-      if (WAB_ROLL_STORE != 0 && (t & 1)) L.stream = L0.stream2;                             \
-      uint32_t* prev = lds + ((t & 1) ? L0.stream : L0.stream2);                             \
-      uint8_t* prev_planes = p.planes ? p.planes - (int64_t)p.B * p.OB : nullptr;            \
-      c.prev_planes = prev_planes;                                                           \
-      c.prev_stream = (WAB_ROLL_STORE == 2 && t > 0) ? prev : nullptr;                       \
-      Params pp = p;                                                                         \
-      pp.planes = prev_planes;                                                               \
-      if (WAB_ROLL_STORE == 1 && t > 0 && pp.planes) store_units_of<0, 3>(pp, prev, threadIdx.x); \
-      if (WAB_ROLL_FLOOR) {  /* A/B floor: the stores alone (results wrong by design) */    \
+      if (t & 1) L.stream = L0.stream2;                                                      \
+      c.prev_planes = p.planes ? p.planes - (int64_t)p.B * p.OB : nullptr;                   \
+      c.prev_stream = t > 0 ? lds + ((t & 1) ? L0.stream : L0.stream2) : nullptr;           \
+      if (WAB_ROLL_FLOOR) {  /* diagnostic floor: the stores alone (results wrong by design) */ \
         lds_barrier();                                                                       \
         lds_barrier();                                                                       \
       } else {                                                                               \
         __VA_ARGS__;                                                                         \
       }                                                                                      \
       if (FEAT) step_features<true>(p, L, lds, wave, lane, t);  /* this step's rows */     \
-      if (WAB_ROLL_STORE == 1 && t > 0 && pp.planes) store_units_of<3, 6>(pp, prev, threadIdx.x); \
-      if (WAB_ROLL_STORE == 0) {                                                             \
-        if (p.planes) store_obs<true>(p, lds + L.stream, threadIdx.x);                       \
-      } else if (t == T - 1 && p.planes) {                                                   \
+      if (t == T - 1 && p.planes) {                                                          \
         lds_barrier();                                                                       \
         store_units_of<0, 6>(p, lds + L.stream, threadIdx.x);                                \
       }                                                                                      \
@@ -1682,9 +1513,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     if (wave == 0) {
       CarryW0 c;
       WAB_ROLL_STEP({
-        WAB_PRIO(true, 3);
+        __builtin_amdgcn_s_setprio(3);
         bushes_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
-        WAB_PRIO(true, 0);
+        __builtin_amdgcn_s_setprio(0);
       })
     } else if (wave == 1) {
       CarryPtr<CarryHdr> c;
@@ -1694,7 +1525,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
       WAB_ROLL_STEP((wolves_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1)))
     } else {
       CarryPtr<CarryHdr> c;
-      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1, c.prev_planes, c.prev_stream)))
+      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1)))
     }
 #undef WAB_ROLL_STEP
   }

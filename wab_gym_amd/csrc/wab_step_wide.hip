@@ -46,9 +46,7 @@ namespace wab {
 #define WIDE_STAMP(slot) do {} while (0)
 #endif
 
-#ifndef WAB_WIDE_SPEC  // wolf slots W0 loads with the state, before the count is known
-#define WAB_WIDE_SPEC 8
-#endif
+constexpr int kWideSpec = 8;  // wolf slots W0 loads with the state, before the count is known
 
 namespace {
 
@@ -217,9 +215,9 @@ __device__ __forceinline__ uint32_t chunk_bits(const Params& p, const uint32_t* 
 // one thread in program order.
 constexpr uint32_t kObsThreads = 192;
 
-__device__ __forceinline__ void store16(const Params& p, uint8_t* out, uint32_t q, const u32x4& v) {
-  if (p.obs_nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out) + q);
-  else reinterpret_cast<u32x4*>(out)[q] = v;
+// plain stores: measured faster than non-temporal ones for this pattern
+__device__ __forceinline__ void store16(const Params&, uint8_t* out, uint32_t q, const u32x4& v) {
+  reinterpret_cast<u32x4*>(out)[q] = v;
 }
 
 // 16 bits of row chunk r (< WC) of one plane's rows
@@ -289,11 +287,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const Params p = kernel_params(p0);  // (re-read per wave branch and phase below)
   const WideLayout L = wide_layout(p);
-#ifdef WAB_WIDE_ROT  // diagnostic: rotate the workgroup -> env-chunk mapping (XCD vs address effects)
-  const int64_t g0 = (int64_t)((blockIdx.x + WAB_WIDE_ROT) % gridDim.x) * 64;
-#else
   const int64_t g0 = (int64_t)blockIdx.x * 64;
-#endif
   if (g0 >= p.B) return;  // (uniform over the workgroup)
 #ifdef WAB_STAMPS
   if (threadIdx.x == 0 && p.stamps) {  // kernel entry (slot 32) and the XCD (slot 33)
@@ -348,7 +342,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
       if (active) {
         food = p.food[g];
 #pragma unroll
-        for (int k = 0; k < WAB_WIDE_SPEC && k < SLOTS; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
+        for (int k = 0; k < kWideSpec && k < SLOTS; ++k) wr[k] = p.wolves[(int64_t)k * p.B + g];  // speculatively
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (i < p.eaten_cap) {
@@ -362,7 +356,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
       ndep = (int)misc_ndep(h.hdr.z);
       const int status_old = (int)misc_status(h.hdr.z);
 #pragma unroll
-      for (int k = WAB_WIDE_SPEC; k < SLOTS; ++k)
+      for (int k = kWideSpec; k < SLOTS; ++k)
         if (k < nw) wr[k] = p.wolves[(int64_t)k * p.B + g];
 #pragma unroll
       for (int k = 0; k < SLOTS; ++k) opaque(wr[k]);  // (loaded on some paths only: settle it here)
@@ -521,7 +515,7 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
         blk[1] = (uint32_t)jm;
         blk[2] = (uint32_t)(jm >> 32);
       }
-      setprio_age(p);
+      __builtin_amdgcn_s_setprio(0);
       WIDE_STAMP(3);
       obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       WIDE_STAMP(4);
@@ -655,11 +649,11 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
           cv = (uint32_t)bush_value_fast(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1),
                                          p.bush_power);
         cval[lane] = cv;
-        setprio_age(p);
+        __builtin_amdgcn_s_setprio(0);
       } else {
         // ---------------------------------------------- W3 P0: the ostrich grids; W2 P0: ring
         // offsets and gap table -> LDS, the spawn set (spawn_wolves :527-576)
-        setprio_age(p);
+        __builtin_amdgcn_s_setprio(0);
         // the ostrich grids in two halves: W3 from the start, W2 after its ring word (it would
         // otherwise wait ~10 us at B1 while W3 alone issues them: 46.9 -> 46.3 us)
         if (wave == 3) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
@@ -900,38 +894,16 @@ __device__ __forceinline__ void slot_set(uint32_t (&wr)[SLOTS], int k, uint32_t 
   for (int j = 0; j < SLOTS; ++j) wr[j] = j == k ? v : wr[j];
 }
 
-// WAB_WIDE_ROLL_LINES (multi-step launches): 1 = each step's obs as whole 128-byte lines, the
-// group's chunk in address order by all 256 threads after B2 (lines that touch a done env after
-// its new episode, B4); 0 = plane by plane as soon as each plane is final (the per-step kernel's
-// order: a line at a plane or env boundary is then written in two parts, microseconds apart).
+// Multi-step launches store each step's obs as whole 128-byte lines, the group's chunk in
+// address order by all 256 threads after B2 (lines that touch a done env after its new episode,
+// B4), not plane by plane as the per-step kernel does (a line at a plane or env boundary is then
+// written in two parts, microseconds apart: 60.3 against 42.9 us per step into a rollout buffer).
 // Every store instruction must cover whole lines: a fixed chunk per thread over the envs (each
 // instruction 1 KiB contiguous, but an env-boundary line split between two instructions)
 // measured 49.9 us against 43.1 (profiles/r03_wideroll/ab_fixed/).
-#ifndef WAB_WIDE_ROLL_LINES
-#define WAB_WIDE_ROLL_LINES 1
-#endif
 
-
-// the group's obs chunks (16 bytes) whose 128-byte line touches a done env (jm) iff `touching`,
-// from bm / wp (the step's snapshot S, or a done env's new episode) and the fixed ostrich grid
-__device__ __forceinline__ void obs_lines(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
-                                          uint32_t n_active, unsigned long long jm, bool touching, int tid) {
-  const uint32_t CPE = (uint32_t)p.OB >> 4;  // chunks per env (the group's chunk starts line-aligned:
-                                             // 64 * OB and B * OB are multiples of 128)
-  const uint32_t n = n_active * CPE;
-  uint32_t e = 0, r = (uint32_t)tid;
-  while (r >= CPE) { r -= CPE; ++e; }
-  for (uint32_t c = (uint32_t)tid; c < n; c += 256u) {
-    const uint32_t c0 = c & ~7u, c1 = min(c0 + 7u, n - 1u);  // the line's chunks
-    const uint32_t e0 = __umulhi(c0, p.magic_CPE), e1 = __umulhi(c1, p.magic_CPE);  // (c < 2^16: exact)
-    const bool t = ((jm >> e0) | (jm >> e1)) & 1ull;
-    if (t == touching) store16(p, out, c, expand16(chunk_bits(p, bm, wp, e, r)));
-    r += 256u;
-    while (r >= CPE) { r -= CPE; ++e; }
-  }
-}
-
-// obs_lines by rows: thread q of the group's 3 W rows per env stores its row's CPR chunks with
+// The group's obs rows whose 128-byte line touches a done env (jm) iff `touching`: thread q of
+// the group's 3 W rows per env stores its row's CPR chunks with
 // consecutive instructions (one row read, one plane / row decode per row instead of per chunk);
 // for CPR = 2 an instruction covers every other 16 bytes and the next one the rest, so each
 // line is whole within two back-to-back instructions of one wave (merged in L2).  Envs that are
@@ -964,40 +936,6 @@ __device__ __forceinline__ void obs_rows(const Params& p, const uint32_t* bm, co
   }
 }
 
-// S as soon as it is complete (B1) by the threads of W1..W3, every row whatever the env's fate;
-// after B4 the same threads (same mapping: program order per address) rewrite the rows of the
-// done envs with their new episode (those few lines are then written twice, the rest whole once)
-__device__ __forceinline__ void obs_rows_b1(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
-                                            uint32_t n_active, unsigned long long jm, bool jobs_only, int idx) {
-  constexpr uint32_t NT = 192;
-  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W;
-  const uint32_t RPE = 3u * W;
-  const uint32_t nr = n_active * RPE;
-  const uint32_t ost = 1u << p.ch;
-  uint32_t e = 0, rr = (uint32_t)idx;
-  while (rr >= RPE) { rr -= RPE; ++e; }
-  for (uint32_t q = (uint32_t)idx; q < nr; q += NT) {
-    if (!jobs_only || ((jm >> e) & 1ull)) {
-      const uint32_t k = (rr >= W ? 1u : 0u) + (rr >= 2u * W ? 1u : 0u);
-      const uint32_t i = rr - k * W;
-      const uint32_t c = e * CPE + rr * CPR;
-      const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? ost : 0u) : (k == 0u ? wp : bm)[e * kWidePitch + i];
-      store16(p, out, c, expand16(v & 0xFFFFu));
-      if (CPR == 2u) store16(p, out, c + 1u, expand16(v >> 16));
-    }
-    rr += NT;
-    while (rr >= RPE) { rr -= RPE; ++e; }
-  }
-}
-#ifndef WAB_WIDE_S_AFTER_B1  // 1: obs_rows_b1 after B1 and for the done envs after B4 (A/B)
-#define WAB_WIDE_S_AFTER_B1 0
-#endif
-// 1: the workgroups of every other 256-block (which share CUs with the others) store S after
-// B1, the rest after B2, so that the workgroups of a CU do not all store at once (A/B)
-#ifndef WAB_WIDE_S_MIX
-#define WAB_WIDE_S_MIX 0
-#endif
-
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
 // (tools/phase_stamps.py --rollout T --config wide31): W0 0..7, W1 8..13, W2 16..20, W3 24..27,
 // the done-env section 36..39
@@ -1011,13 +949,6 @@ __device__ __forceinline__ void obs_rows_b1(const Params& p, const uint32_t* bm,
 #define ROLLW_STAMP(slot) do {} while (0)
 #endif
 
-#ifndef WAB_WIDE_STRIP_W3  // multi-step launches: W3 draws the entering strip for W1 (A/B)
-#define WAB_WIDE_STRIP_W3 1
-#endif
-
-#ifndef WAB_WIDE_ROW_STORES  // 1: obs_rows, 0: obs_lines (A/B)
-#define WAB_WIDE_ROW_STORES 1
-#endif
 #ifndef WAB_WIDE_ROLL_FLOOR  // diagnostic: every step's work skipped, its obs stores kept
 #define WAB_WIDE_ROLL_FLOOR 0
 #endif
@@ -1036,21 +967,6 @@ __device__ __forceinline__ void wide_step_slice(Params& p, int t) {
 
 }  // namespace
 
-// Multi-step launches (A/B, WAB_ROLL_STAGGER_NS > 0): the four workgroups that share a CU
-// (blockIdx 256 apart) start their first step k * STAGGER ns apart, k = blockIdx >> 8 & 3, so
-// that their store phases do not coincide (they otherwise stay in phase: they share one drain)
-#ifndef WAB_ROLL_STAGGER_NS
-#define WAB_ROLL_STAGGER_NS 0
-#endif
-__device__ __forceinline__ void roll_stagger() {
-  if (WAB_ROLL_STAGGER_NS > 0) {
-    const uint64_t k = (blockIdx.x >> 8) & 3u;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    const uint64_t until = t0 + k * (uint64_t)(WAB_ROLL_STAGGER_NS / 10);
-    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
-  }
-}
-
 template <int SLOTS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wab_rollout_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1058,8 +974,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   if (g0 >= p0.B) return;  // (uniform over the workgroup)
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int T = p0.n_steps;
-  roll_stagger();
-  const bool s_b1 = WAB_WIDE_S_AFTER_B1 || (WAB_WIDE_S_MIX && ((blockIdx.x >> 8) & 1u));  // (uniform)
   const int n_active = (int)min((int64_t)64, p0.B - g0);
   const int64_t g = g0 + lane;
   const bool active = lane < n_active;
@@ -1129,7 +1043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     const WHead h = whead_of(p, g, active, hdr, a);
     if (WAB_WIDE_ROLL_FLOOR) {  // (A/B floor: the stores alone; results wrong by design)
       lds_barrier();
-      (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid);
+      obs_rows(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid);
       lds_barrier();
       continue;
     }
@@ -1239,11 +1153,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         }
       }
       kill = kill && !p.god_mode;
-      if (!WAB_WIDE_ROLL_LINES) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        obs_plane<0>(p, wp, out, (uint32_t)n_active, lane);
-      }
       ROLLW_STAMP(1);
       // emptied tiles that scrolled back into view are absent from S (:506): cleared from the
       // bitmap once W1 has scrolled it (the per-step kernel's W1 does this from its own loads)
@@ -1364,13 +1273,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         blk[2] = (uint32_t)(jm >> 32);
       }
       __builtin_amdgcn_s_setprio(0);
-      if (!WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       ROLLW_STAMP(4);
       lds_barrier();  // B2
       ROLLW_STAMP(5);
-      if (WAB_WIDE_ROLL_LINES && !s_b1)  // S of the lines without a done env (the rest after B4)
-        (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
-                  false, tid);
+      // S of the lines without a done env (the rest after B4)
+      obs_rows(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+               false, tid);
       ROLLW_STAMP(6);
       // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
       if (active && !job) {
@@ -1467,18 +1375,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
           if (lane == 0) bush_thr_pads(thr, nthr);
           __builtin_amdgcn_s_waitcnt(0);
-        } else if (WAB_WIDE_ROLL_LINES) {  // the last step's eaten-empty tile (its S obs are stored)
+        } else {  // the last step's eaten-empty tile (its S obs are stored)
           const unsigned long long jmp = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
           if (lane < n_active && !((jmp >> lane) & 1ull) && (info[lane] & 2u))
             bm[me + (uint32_t)p.cw] &= ~(1u << p.ch);
         }
-        uint32_t strip;
-        if (WAB_WIDE_STRIP_W3) {  // drawn by W3 meanwhile (flag[1] = t + 1)
-          lds_await_step(p, flag + 1, (uint32_t)t + 1u);
-          strip = wstrip[lane];
-        } else {
-          strip = active ? strip_bits(p, h) : 0u;
-        }
+        lds_await_step(p, flag + 1, (uint32_t)t + 1u);  // the strip, drawn by W3 meanwhile
+        const uint32_t strip = wstrip[lane];
         const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
         const uint32_t top = 1u << (p.H - 1);
         const int Wv = p.W;
@@ -1522,13 +1425,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         ROLLW_STAMP(10);
       } else {
         // ---------------------------------------------- W3: ostrich grids; W2: tables, spawn set
-        if (wave == 3 && WAB_WIDE_STRIP_W3) {  // the entering strip's draws, for W1's scroll
+        if (wave == 3) {  // the entering strip's draws, for W1's scroll
           wstrip[lane] = active ? strip_bits(p, h) : 0u;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
           if (lane == 0) lds_publish_step(flag + 1, (uint32_t)t + 1u);
         }
-        if (wave == 3 && !WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 0u, 4u);
         if (wave == 2) {
           if (t == 0) {
             copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
@@ -1542,20 +1444,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
               spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
             });
-          if (!WAB_WIDE_ROLL_LINES) obs_plane2(p, out, (uint32_t)n_active, lane, 4u, 8u);
           ROLLW_STAMP(17);
         }
       }
       lds_barrier();  // B1
       ROLLW_STAMP(8 * wave + (wave == 1 ? 3 : 2));
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
-      if (WAB_WIDE_ROLL_LINES && s_b1) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid - 64);
-      if (wave < 3 && !WAB_WIDE_ROLL_LINES) obs_plane<1>(p, bm, out, (uint32_t)n_active, tid);
       lds_barrier();  // B2
       ROLLW_STAMP(8 * wave + (wave == 1 ? 4 : 3));
-      if (WAB_WIDE_ROLL_LINES && !s_b1)
-        (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
-                  false, tid);
+      obs_rows(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
+               false, tid);
       ROLLW_STAMP(8 * wave + (wave == 1 ? 5 : 4));
     }
 
@@ -1563,8 +1461,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     const int n_jobs = (int)blk[0];
     const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
     // ------------------------------------------------ P2: the continuing envs' bitmaps (post-eat)
-    if (!WAB_WIDE_ROLL_LINES && tid < n_active && !((jmask >> tid) & 1ull) && (info[tid] & 2u))
-      bm[(uint32_t)tid * P + (uint32_t)p.cw] &= ~(1u << p.ch);  // eaten empty (LINES: by W1, next step)
+    // (the continuing envs' eaten-empty tiles are cleared from bm by W1 at the next step's start)
     if (wave == 0) {
       if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
       if (lane == 0 && n_jobs) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);
@@ -1650,13 +1547,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food2;
         }
       }
-      if (WAB_WIDE_ROLL_LINES && s_b1) {  // the done envs' rows, by their S writers
-        if (wave > 0) obs_rows_b1(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid - 64);
-      } else if (WAB_WIDE_ROLL_LINES) {  // the lines that touch a done env: its new episode, its neighbours' S
-        (WAB_WIDE_ROW_STORES ? obs_rows : obs_lines)(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
-      }
-      else
-        for (int jj = 0; jj < n_jobs; ++jj) obs_env(p, bm, wp, out, jobEnv[jj], tid);  // (plane 2 is already right)
+      // the lines that touch a done env: its new episode, its neighbours' S
+      obs_rows(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
     }
     if (wave == 0) ROLLW_STAMP(39);
     if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
@@ -1666,7 +1558,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         const uint32_t e = u >> 5, i = u & 31u;
         if ((int)e >= n_active || i >= (uint32_t)p.W) continue;
         uint32_t v = bm[e * P + i];
-        if (WAB_WIDE_ROLL_LINES && !((jmask >> e) & 1ull) && (info[e] & 2u) && i == (uint32_t)p.cw) v &= ~(1u << p.ch);
+        if (!((jmask >> e) & 1ull) && (info[e] & 2u) && i == (uint32_t)p.cw) v &= ~(1u << p.ch);
         p.bushmap[(size_t)(g0 + e) * 32u + i] = v;
       }
     }
