@@ -240,14 +240,13 @@ def rollout_wide_report(env, st, g, launches, T):
 
     B = env.num_envs
     nb = (B + 63) // 64
-    seqs = {"W0": [0, 1, 2, 3, 4, 5, 6, 7], "W1": [8, 9, 10, 11, 12, 13], "W2": [16, 17, 18, 19, 20],
-            "W3": [24, 26, 27, 28], "jobs (W0)": [37, 39]}
+    seqs = {"W0": [0, 1, 2, 3, 4, 5, 39], "W1": [8, 9, 10, 11, 12], "W2": [16, 17, 18, 19, 20],
+            "W3": [24, 25, 26, 27, 28]}
     names = {"W0": ["start", "despawn/pursuit/grid", "emptied clear + log -> B1", "after B1", "eat/done -> B2",
-                    "after B2", "S rows stored", "P2 (spawns, state)"],
-             "W1": ["start", "scroll (flag)", "tile value", "after B1", "after B2", "S rows stored"],
-             "W2": ["start", "spawn set", "after B1", "after B2", "S rows stored"],
-             "W3": ["start", "after B1", "after B2", "S rows stored"],
-             "jobs (W0)": ["after B4", "new-episode obs stored"]}
+                    "after B2", "P2 + new episodes"],
+             "W1": ["start", "scroll (flag)", "tile value", "after B1", "after B2"],
+             "W2": ["start", "spawn set", "stores -> B1", "stores -> B2", "the rest stored"],
+             "W3": ["start", "strip", "stores -> B1", "stores -> B2", "the rest stored"]}
     acc = {k: [] for k in seqs}
     for it in range(launches):
         st.zero_()

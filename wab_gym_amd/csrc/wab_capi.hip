@@ -59,6 +59,7 @@ struct wab_handle {
   bool small_g11 = false;    // the small kernel's 11x11 specialisation (geometry_11)
   wab::RewardTable rewards;  // exact doubles of the rewards a step returns (n = 0: ambiguous)
   size_t wide_lds_bytes = 0;  // LDS per workgroup of the wide kernel (see wab_create)
+  size_t wide_roll_lds_bytes = 0;  // ... of its multi-step build (wab_rollout_wide)
 };
 
 namespace {
@@ -148,8 +149,9 @@ bool small_view(const Params& p) {
 bool geometry_11(const Params& p) { return p.W == 11 && p.H == 11 && p.S == 11 && p.margin == 1; }
 
 bool wide_view(const Params& p) {
-  return !small_view(p) && p.W <= 32 && p.H <= 32 && (p.S == 16 || p.S == 32) && p.S >= p.H &&
-         !p.restrict_view && wab::wide_layout(p).total * 4u <= 64u * 1024u;
+  return !small_view(p) && p.W <= 31 && p.H <= 32 && (p.S == 16 || p.S == 32) && p.S >= p.H &&
+         !p.restrict_view && wab::wide_layout(p).total * 4u <= 64u * 1024u &&
+         wab::wide_roll_layout(p).total * 4u <= 64u * 1024u;
 }
 
 // the wide kernel holds kWideRegSlots wolves per env in registers whatever wolf_slots is; a lane
@@ -587,10 +589,13 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes);
   if (h->step_kernel == KERNEL_WIDE) {
     h->wide_lds_bytes = (size_t)wab::wide_layout(p).total * 4u;
-    for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots),
-                    reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots>)})
+    h->wide_roll_lds_bytes = (size_t)wab::wide_roll_layout(p).total * 4u;
+    for (void* k : {wide_kernel_ptr<0>(slots), wide_kernel_ptr<1>(slots)})
       if (e == hipSuccess)
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_lds_bytes);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_roll_lds_bytes);
   }
   if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
     for (void* k : {h->small_g11 ? small_kernel_ptr<11>(slots) : small_kernel_ptr<0>(slots),
@@ -659,6 +664,17 @@ int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* re
     p.t_status = terminal->status;
   }
   DeviceGuard guard(h->device);
+  if (h->step_kernel == KERNEL_WIDE && !p.t_planes && ((size_t)p.B * (size_t)p.OB) % 16u == 0) {
+    // the wide view without terminal obs: the rollout build with one step (its obs as whole
+    // 128-byte lines in address order after the step; the per-step kernel stores each plane as
+    // soon as it is final, a line at a plane or env boundary in two parts)
+    if (h->n_blocks == 0) return WAB_OK;
+    p.n_steps = 1;
+    hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_roll_lds_bytes,
+                       (hipStream_t)stream, p);
+    HIP_TRY(hipGetLastError());
+    return WAB_OK;
+  }
   return launch<0>(h, p, (hipStream_t)stream);
 }
 
@@ -686,7 +702,7 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
     DeviceGuard guard(h->device);
     if (h->step_kernel == KERNEL_WIDE) {
       if (h->n_blocks == 0) return WAB_OK;
-      hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_lds_bytes,
+      hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_roll_lds_bytes,
                          (hipStream_t)stream, p);
       HIP_TRY(hipGetLastError());
       return WAB_OK;

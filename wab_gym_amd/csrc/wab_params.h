@@ -211,13 +211,8 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
 // env-major with a 33-dword pitch so that lanes (= envs) touching the same row hit
 // different banks (dwords)
 constexpr uint32_t kWidePitch = 33;
-constexpr int kWideLdsLog = 16;  // multi-step launches: eaten-log entries W0 keeps on chip (0..3 in
-                                 // registers, 4..15 in LDS; later ones, rare, in HBM)
 struct WideLayout {
   uint32_t bm, wp, spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey;
-  uint32_t nhdr, act, flag;  // multi-step launches: next headers (W0), next actions, W1 -> W0 flag
-  uint32_t elxy, elrem;      // multi-step launches: eaten-log entries 4..kWideLdsLog-1 (W0)
-  uint32_t wstrip;           // multi-step launches: the entering strip's bits (W3 -> W1)
   uint32_t total;
 };
 
@@ -238,11 +233,48 @@ __host__ __device__ inline WideLayout wide_layout(const Params& p) {
   L.blk = o; o += 4u;                         // n_jobs, job mask lo, hi
   L.jobEnv = o; o += 64u;
   L.jobKey = o; o += 128u;
+  L.total = o;
+  return L;
+}
+
+// LDS of the wide view's multi-step build (wab_rollout_wide): the view bitmaps and wolf grids
+// twice (step t builds its obs in buffer t & 1 while the store waves write step t - 1's from
+// the other), at a 31-dword pitch (W <= 31: odd viewports; odd, so lanes = envs still hit
+// distinct banks), plus the state the waves carry between steps.  At 31x31 it is ~39 KB, so
+// that four workgroups (B = 65536: all 1024 at once) fit a CU's 160 KB.
+constexpr uint32_t kRollPitch = 31;
+constexpr int kWideRollLog = 8;  // eaten-log entries W0 keeps on chip (0..3 in registers, 4..7 in
+                                 // LDS; later ones, rare, in HBM)
+struct WideRollLayout {
+  uint32_t bm[2], wp[2], spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey;
+  uint32_t nhdr, act, flag;  // next headers (W0), next actions (W3), hand-off flags
+  uint32_t elxy, elrem;      // eaten-log entries 4..kWideRollLog-1 (W0)
+  uint32_t wstrip;           // the entering strip's bits (W3 -> W1)
+  uint32_t total;
+};
+
+__host__ __device__ inline WideRollLayout wide_roll_layout(const Params& p) {
+  WideRollLayout L;
+  uint32_t o = 0;
+  for (int b = 0; b < 2; ++b) {
+    L.bm[b] = o; o += lds_align4(64u * kRollPitch);
+    L.wp[b] = o; o += lds_align4(64u * kRollPitch);
+  }
+  L.spw = (((uint32_t)p.R + 31u) >> 5) | 1u;
+  L.spawn = o; o += lds_align4(64u * L.spw);
+  L.ring = o; o += lds_align4((uint32_t)p.R);
+  L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));
+  L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));
+  L.cval = o; o += 64u;
+  L.info = o; o += 64u;
+  L.blk = o; o += 4u;
+  L.jobEnv = o; o += 64u;
+  L.jobKey = o; o += 128u;
   L.nhdr = o; o += 64u * 4u;                  // uint4 per env
   L.act = o; o += 16u;                        // 64 int8 actions
-  L.flag = o; o += 4u;
-  L.elxy = o; o += 64u * (uint32_t)(kWideLdsLog - 4);      // [entry - 4][env] tiles
-  L.elrem = o; o += 16u * (uint32_t)(kWideLdsLog - 4);     // [entry - 4][env] berries left (bytes)
+  L.flag = o; o += 4u;  // [0] W1's scroll, [1] W3's strip, [2] W0 at B1 / B2 (step-tagged values)
+  L.elxy = o; o += 64u * (uint32_t)(kWideRollLog - 4);   // [entry - 4][env] tiles
+  L.elrem = o; o += 16u * (uint32_t)(kWideRollLog - 4);  // [entry - 4][env] berries left (bytes)
   L.wstrip = o; o += 64u;
   L.total = o;
   return L;

@@ -809,23 +809,36 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
 // --------------------------------------------------------------------------- multi-step launches
 // wab_rollout on the wide kernel: each workgroup takes its 64 envs through Params::n_steps steps
 // in one launch (the envs of a workgroup depend on nothing outside it).  The phases of a step
-// are those of wab_step_wide<MODE_STEP>; what changes is where the state lives between steps:
+// are those of wab_step_wide<MODE_STEP>; what changes is where the state lives between steps
+// and when the obs go out:
 //   - every wave: the env's header (W0 writes the next one to LDS, nhdr) and the next step's
 //     actions (W3 prefetches them with one scalar load per group into LDS, act);
 //   - W0: food, the 8 register wolf slots (uncompacted, with a live mask; the rarely used rows
 //     8.. stay in HBM, compacted at rows 8..8+nsp-1, read and written by the env's own lane) and
-//     the first four eaten-log entries (entries >= 4 in HBM, own lane);
-//   - W1: the view bitmap stays in LDS (bm), post-eat, new episodes' rows included.
-// Only step 0 loads state and only the last step stores it: after step 0 no wave issues a
-// vector load on its common path, so nothing waits for the previous steps' obs stores, and a
-// step's obs drain overlaps the next step's dynamics.  W0 (which owns the eaten log) clears the
-// emptied tiles that scrolled back into view from the bitmap after W1's scroll (LDS flag; the
-// per-step kernel has W1 do it from its own loads of the log).  Co-located wolves are
-// interchangeable (their despawn keys are (tile, occurrence index) whatever their order), so
-// the uncompacted slots step exactly as the per-step kernel's compacted rows do.
+//     the first eaten-log entries (0..3 in registers, 4..7 in LDS, later ones in HBM, own lane);
+//   - the view bitmaps and wolf grids live in LDS twice: step t builds its obs (S for the
+//     continuing envs, the new episode for the done ones) in buffer t & 1 -- W1 scrolls the
+//     other buffer's bitmaps into it, W0 draws the wolf grids -- while W2 and W3 store step
+//     t - 1's obs from the other buffer.
+// Obs stores.  A step's obs are 64 x 3 W rows of S bytes; the store waves write them as whole
+// 128-byte lines in address order (thread q of 128 the rows q + 128 k, both halves of a 32-byte
+// row from two back-to-back instructions: each wave-instruction pair covers 16 whole lines).
+// They store while the compute waves work: up to B1 until W0 signals that it reached B1, up to
+// B2 likewise, and after B2 whatever is left, so the compute of step t overlaps the drain of
+// step t - 1 and no barrier waits for more than two rows of issue.  (The round-3 build stored
+// each step's rows after its own B2, all 256 threads, then the done envs' lines after their new
+// episodes: 41.5-46.1 us per step, a workgroup blocked on store issue for most of its step and
+// the four workgroups of a CU in phase.)  Only step 0 loads state and only the last step stores
+// it; W1 and W0 issue no vector load after step 0 on their common path.  The last step's obs
+// go out after it by all 256 threads.  W0 (which owns the eaten log) clears the emptied tiles
+// that scrolled back into view after W1's scroll (LDS flag); the eaten-empty centre bit of a
+// continuing env (post-eat) is applied by W1 when it scrolls that bitmap in the next step.
+// Co-located wolves are interchangeable (their despawn keys are (tile, occurrence index)
+// whatever their order), so the uncompacted slots step exactly as the per-step kernel's
+// compacted rows do.
 namespace {
 
-// W1 -> W0 in step t: the scroll of step t is in bm (value t + 1: no clearing between steps)
+// a step-tagged hand-off: the producer stores a value that grows every step (no clearing)
 __device__ __forceinline__ void lds_publish_step(uint32_t* flag, uint32_t v) {
   __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -835,6 +848,9 @@ __device__ __forceinline__ void lds_await_step(const Params& p, const uint32_t* 
     __builtin_amdgcn_s_sleep(1);
   }
   atomicAdd(&p.counters[CTR_HANDOFF_TIMEOUTS], 1ull);
+}
+__device__ __forceinline__ bool lds_reached(const uint32_t* flag, uint32_t v) {  // (wave-uniform)
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= v;
 }
 
 // whead of a carried header and action
@@ -894,46 +910,35 @@ __device__ __forceinline__ void slot_set(uint32_t (&wr)[SLOTS], int k, uint32_t 
   for (int j = 0; j < SLOTS; ++j) wr[j] = j == k ? v : wr[j];
 }
 
-// Multi-step launches store each step's obs as whole 128-byte lines, the group's chunk in
-// address order by all 256 threads after B2 (lines that touch a done env after its new episode,
-// B4), not plane by plane as the per-step kernel does (a line at a plane or env boundary is then
-// written in two parts, microseconds apart: 60.3 against 42.9 us per step into a rollout buffer).
-// Every store instruction must cover whole lines: a fixed chunk per thread over the envs (each
-// instruction 1 KiB contiguous, but an env-boundary line split between two instructions)
-// measured 49.9 us against 43.1 (profiles/r03_wideroll/ab_fixed/).
+// A thread's position in a finished step's obs rows: row q (of the group's 3 W rows per env,
+// in address order) is row rr of env e
+struct RowCursor {
+  uint32_t q, e, rr;
+};
+__device__ __forceinline__ RowCursor row_cursor(const Params& p, uint32_t q) {
+  const uint32_t RPE = 3u * (uint32_t)p.W;
+  RowCursor c;
+  c.q = q;
+  c.e = q / RPE;
+  c.rr = q - c.e * RPE;
+  return c;
+}
 
-// The group's obs rows whose 128-byte line touches a done env (jm) iff `touching`: thread q of
-// the group's 3 W rows per env stores its row's CPR chunks with
-// consecutive instructions (one row read, one plane / row decode per row instead of per chunk);
-// for CPR = 2 an instruction covers every other 16 bytes and the next one the rest, so each
-// line is whole within two back-to-back instructions of one wave (merged in L2).  Envs that are
-// neither done nor next to a done env skip the line test.
-__device__ __forceinline__ void obs_rows(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
-                                         uint32_t n_active, unsigned long long jm, bool touching, int tid) {
-  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W;
-  const uint32_t RPE = 3u * W;  // rows per env
-  const uint32_t n = n_active * CPE, nr = n_active * RPE;
-  const unsigned long long jn = jm | (jm << 1) | (jm >> 1);  // done envs and their neighbours
-  const uint32_t ost = 1u << p.ch;  // the ostrich grid's row cw
-  uint32_t e = 0, rr = (uint32_t)tid;
-  while (rr >= RPE) { rr -= RPE; ++e; }
-  for (uint32_t q = (uint32_t)tid; q < nr; q += 256u) {
-    const uint32_t k = (rr >= W ? 1u : 0u) + (rr >= 2u * W ? 1u : 0u);
-    const uint32_t i = rr - k * W;
-    const uint32_t c = e * CPE + rr * CPR;  // the row's first chunk
-    bool t = false;
-    if ((jn >> e) & 1ull) {
-      const uint32_t c0 = c & ~7u, c1 = min(c0 + 7u, n - 1u);
-      t = ((jm >> __umulhi(c0, p.magic_CPE)) | (jm >> __umulhi(c1, p.magic_CPE))) & 1ull;
-    }
-    if (t == touching) {
-      const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? ost : 0u) : (k == 0u ? wp : bm)[e * kWidePitch + i];
-      store16(p, out, c, expand16(v & 0xFFFFu));
-      if (CPR == 2u) store16(p, out, c + 1u, expand16(v >> 16));
-    }
-    rr += 256u;
-    while (rr >= RPE) { rr -= RPE; ++e; }
-  }
+// store obs row c.q (wolf rows wp, bush rows bm at kRollPitch; the ostrich grid is the centre
+// cell alone) and move the cursor NT rows on
+template <uint32_t NT>
+__device__ __forceinline__ void roll_store_row(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                               RowCursor& c) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W, RPE = 3u * W;
+  const uint32_t k = (c.rr >= W ? 1u : 0u) + (c.rr >= 2u * W ? 1u : 0u);
+  const uint32_t i = c.rr - k * W;
+  const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? 1u << p.ch : 0u) : (k == 0u ? wp : bm)[c.e * kRollPitch + i];
+  const uint32_t ch0 = c.e * CPE + c.rr * CPR;  // the row's first 16-byte chunk
+  store16(p, out, ch0, expand16(v & 0xFFFFu));
+  if (CPR == 2u) store16(p, out, ch0 + 1u, expand16(v >> 16));
+  c.q += NT;
+  c.rr += NT;
+  while (c.rr >= RPE) { c.rr -= RPE; ++c.e; }
 }
 
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
@@ -977,7 +982,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   const int n_active = (int)min((int64_t)64, p0.B - g0);
   const int64_t g = g0 + lane;
   const bool active = lane < n_active;
-  constexpr uint32_t P = kWidePitch;
+  constexpr uint32_t P = kRollPitch;
   const uint32_t me = (uint32_t)lane * P;
 
   // carried state (per wave: the header; W0: food, wolves, eaten log)
@@ -989,22 +994,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   uint32_t live = 0;  // occupied register slots
   int nsp = 0;        // wolves in HBM rows SLOTS..SLOTS+nsp-1
   uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
-  {  // the W1 -> W0 and W3 -> W1 step flags start below every step's value
-    const WideLayout L = wide_layout(p0);
-    if (tid == 0) {
-      lds[L.flag] = 0u;
-      lds[L.flag + 1] = 0u;
-    }
+  {  // the step flags start below every step's value
+    const WideRollLayout L = wide_roll_layout(p0);
+    if (tid < 4) lds[L.flag + tid] = 0u;
     lds_barrier();
   }
 
   for (int t = 0; t < T; ++t) {
     const bool last = t == T - 1;
+    const int cur = t & 1;
     Params p = kernel_params(p0);
     wide_step_slice(p, t);
-    const WideLayout L = wide_layout(p);
-    uint32_t* bm = lds + L.bm;
-    uint32_t* wp = lds + L.wp;
+    const WideRollLayout L = wide_roll_layout(p);
+    // (buffers chosen by selects: a runtime index into the layout would put it in scratch)
+    uint32_t* bm = lds + (cur ? L.bm[1] : L.bm[0]);  // this step's obs: bitmaps and wolf grids
+    uint32_t* wp = lds + (cur ? L.wp[1] : L.wp[0]);
+    uint32_t* bm_prev = lds + (cur ? L.bm[0] : L.bm[1]);  // the last step's (stored during this one)
+    const uint32_t* wp_prev = lds + (cur ? L.wp[0] : L.wp[1]);
     uint32_t* spawn = lds + L.spawn;
     uint32_t* ring = lds + L.ring;
     uint64_t* gap = reinterpret_cast<uint64_t*>(lds + L.gap);
@@ -1020,11 +1026,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     uint32_t* wstrip = lds + L.wstrip;
     uint32_t* elxy = lds + L.elxy;
     uint8_t* elrem = reinterpret_cast<uint8_t*>(lds + L.elrem);
-    // (eaten-log entries 4..kWideLdsLog-1 in LDS, later ones in HBM: rare, a load there waits
-    // for this wave's outstanding stores)
     const uint32_t OB = (uint32_t)p.OB;
     uint8_t* out = p.planes + (size_t)g0 * OB;
+    uint8_t* out_prev = out - (size_t)p.B * OB;  // step t - 1's slice (t > 0)
     const int RW = (p.R + 31) >> 5;
+    // the W0 -> store-wave phase signals of this step (flag[2]): B1 reached, B2 reached
+    const uint32_t at_b1 = 2u * (uint32_t)t + 1u, at_b2 = 2u * (uint32_t)t + 2u;
+    const uint32_t n_rows = (uint32_t)n_active * 3u * (uint32_t)p.W;  // the group's obs rows per step
 
     int a = 0;
     if (t == 0) {
@@ -1041,9 +1049,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       a = (int)reinterpret_cast<const int8_t*>(act)[lane];
     }
     const WHead h = whead_of(p, g, active, hdr, a);
-    if (WAB_WIDE_ROLL_FLOOR) {  // (A/B floor: the stores alone; results wrong by design)
-      lds_barrier();
-      obs_rows(p, bm, wp, out, (uint32_t)n_active, 0ull, false, tid);
+    if (WAB_WIDE_ROLL_FLOOR) {  // (diagnostic floor: the store waves' stores alone; results wrong)
+      RowCursor rc = row_cursor(p, (uint32_t)(tid - 128));
+      if (wave >= 2 && t > 0)
+        while (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
       lds_barrier();
       continue;
     }
@@ -1069,7 +1078,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
               lrem[i] = p.eaten_rem[(int64_t)i * p.B + g];
             }
           const int ne0 = (int)misc_ne(h.hdr.z);  // entries 4.. on chip (step 0: nothing stored yet)
-          for (int i = 4; i < ne0 && i < kWideLdsLog; ++i) {
+          for (int i = 4; i < ne0 && i < kWideRollLog; ++i) {
             elxy[(i - 4) * 64 + lane] = p.eaten_xy[(int64_t)i * p.B + g];
             elrem[(i - 4) * 64 + lane] = p.eaten_rem[(int64_t)i * p.B + g];
           }
@@ -1166,14 +1175,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             if (k < ne && lrem[k] == 0u && abs(ddx) <= p.cw && abs(ddy) <= p.ch)
               bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
           }
-          for (int i = 4; i < ne && i < kWideLdsLog; ++i) {  // (more than 4 eaten tiles: LDS)
+          for (int i = 4; i < ne && i < kWideRollLog; ++i) {  // (more than 4 eaten tiles: LDS)
             if (elrem[(i - 4) * 64 + lane] != 0u) continue;
             const uint32_t tt = elxy[(i - 4) * 64 + lane];
             const int ddx = h.ox - xy_x(tt), ddy = h.oy - xy_y(tt);
             if (abs(ddx) <= p.cw && abs(ddy) <= p.ch) bm[me + (uint32_t)(ddx + p.cw)] &= ~(1u << (ddy + p.ch));
           }
-          if (ne > kWideLdsLog) {  // (rare: the rest in HBM; a load here waits for the stores)
-            for (int i = kWideLdsLog; i < ne; ++i) {
+          if (ne > kWideRollLog) {  // (rare: the rest in HBM)
+            for (int i = kWideRollLog; i < ne; ++i) {
               if (p.eaten_rem[(int64_t)i * p.B + g] != 0) continue;
               const uint32_t tt = p.eaten_xy[(int64_t)i * p.B + g];
               const int ddx = h.ox - xy_x(tt), ddy = h.oy - xy_y(tt);
@@ -1187,17 +1196,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       for (int k = 0; k < 4; ++k)
         if (k < ne && lxy[k] == h.cpos) { found = k; found_rem = (int)lrem[k]; }
       ROLLW_STAMP(2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) lds_publish_step(flag + 2, at_b1);  // (the store waves stop before B1)
       lds_barrier();  // B1
       ROLLW_STAMP(3);
-      // ------------------------------------------------ W0 P1: eat, starve, done; then obs
+      // ------------------------------------------------ W0 P1: eat, starve, done
       double reward = 0.0;
       if (active) {
         const bool center_bush = ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u) != 0u;
         if (center_bush && found < 0 && ne > 4) {
-          for (int i = 4; i < ne && i < kWideLdsLog; ++i)
+          for (int i = 4; i < ne && i < kWideRollLog; ++i)
             if (elxy[(i - 4) * 64 + lane] == h.cpos) { found = i; found_rem = (int)elrem[(i - 4) * 64 + lane]; }
-          if (ne > kWideLdsLog)  // (rare)
-            for (int i = kWideLdsLog; i < ne; ++i)
+          if (ne > kWideRollLog)  // (rare)
+            for (int i = kWideRollLog; i < ne; ++i)
               if (p.eaten_xy[(int64_t)i * p.B + g] == h.cpos) { found = i; found_rem = (int)p.eaten_rem[(int64_t)i * p.B + g]; }
         }
         const int rem = found >= 0 ? found_rem : (center_bush ? (int)cval[lane] : 0);
@@ -1211,7 +1222,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
             for (int k = 0; k < 4; ++k)
               if (found == k) lrem[k] = (uint32_t)(rem - 1);
           } else if (found >= 4) {  // (HBM written through: the state at the launch's end)
-            if (found < kWideLdsLog) elrem[(found - 4) * 64 + lane] = (uint8_t)(rem - 1);
+            if (found < kWideRollLog) elrem[(found - 4) * 64 + lane] = (uint8_t)(rem - 1);
             p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
           } else if (ne < p.eaten_cap) {
             if (ne < 4) {
@@ -1222,7 +1233,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
                   lrem[k] = (uint32_t)(rem - 1);
                 }
             } else {
-              if (ne < kWideLdsLog) {
+              if (ne < kWideRollLog) {
                 elxy[(ne - 4) * 64 + lane] = h.cpos;
                 elrem[(ne - 4) * 64 + lane] = (uint8_t)(rem - 1);
               }
@@ -1272,14 +1283,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         blk[1] = (uint32_t)jm;
         blk[2] = (uint32_t)(jm >> 32);
       }
-      __builtin_amdgcn_s_setprio(0);
       ROLLW_STAMP(4);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) lds_publish_step(flag + 2, at_b2);
       lds_barrier();  // B2
       ROLLW_STAMP(5);
-      // S of the lines without a done env (the rest after B4)
-      obs_rows(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
-               false, tid);
-      ROLLW_STAMP(6);
       // ------------------------------------------------ W0 P2: spawns; the next state of continuing envs
       if (active && !job) {
         int n_unplaced = 0;
@@ -1348,134 +1356,151 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food;
         }
       }
+      __builtin_amdgcn_s_setprio(0);
+    } else if (wave == 1) {
+      // ---------------------------------------------- W1 P0: the view bitmap
+      __builtin_amdgcn_s_setprio(2);
+      // source: the last step's bitmaps (step 0: the state's, loaded into that buffer)
+      uint32_t* src = bm_prev;
+      if (t == 0) {
+        const int nthr = p.max_berries;
+        uint64_t tv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
+        const int64_t ga = active ? g : 0;
+        const uint4* sp = reinterpret_cast<const uint4*>(p.bushmap + (size_t)ga * 32u);
+#pragma unroll 1
+        for (int k = 0; k < 8; k += 2) {  // (step 0 only)
+          const uint4 v0 = sp[k], v1 = sp[k + 1];
+          const uint32_t r[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (4 * k + q < p.W) src[me + (uint32_t)(4 * k + q)] = r[q];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
+        if (lane == 0) bush_thr_pads(thr, nthr);
+        __builtin_amdgcn_s_waitcnt(0);
+      }
+      // the last step's eaten-empty centre tile of a continuing env (its obs were pre-eat S),
+      // applied to the source's centre row as it is read
+      bool eaten_empty = false;
+      if (t > 0) {
+        const unsigned long long jmp = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+        eaten_empty = active && !((jmp >> lane) & 1ull) && (info[lane] & 2u);
+      }
+      const uint32_t ccw = eaten_empty ? ~(1u << p.ch) : ~0u;
+      lds_await_step(p, flag + 1, (uint32_t)t + 1u);  // the strip, drawn by W3 meanwhile
+      const uint32_t strip = wstrip[lane];
+      const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
+      const uint32_t top = 1u << (p.H - 1);
+      const int Wv = p.W, cwv = p.cw;
+      uint32_t prev_old = 0u;                   // the old row i - 1
+      uint32_t nxt = active ? src[me] & (cwv == 0 ? ccw : ~0u) : 0u;  // the old row i
+#pragma unroll 1
+      for (int i0 = 0; i0 < Wv; i0 += 4) {  // scroll (:613-629) + the entering strip
+        uint32_t old[5];
+        old[0] = nxt;
+#pragma unroll
+        for (int q = 1; q < 5; ++q)
+          old[q] = (active && i0 + q < Wv) ? src[me + (uint32_t)(i0 + q)] & (i0 + q == cwv ? ccw : ~0u) : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = i0 + q;
+          if (i >= Wv) break;
+          const uint32_t wi = old[q];
+          const uint32_t prev = q == 0 ? prev_old : old[q - 1];
+          const uint32_t next = old[q + 1];
+          const uint32_t sb = (strip >> i) & 1u;
+          uint32_t v = wi;
+          v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
+          v = h.dir == DIR_LEFT ? (i == Wv - 1 ? strip : next) : v;
+          v = h.dir == DIR_UP ? (((wi << 1) & hmask) | sb) : v;
+          v = h.dir == DIR_DOWN ? ((wi >> 1) | (sb ? top : 0u)) : v;
+          bm[me + (uint32_t)i] = active ? v : 0u;
+        }
+        prev_old = old[3];
+        nxt = old[4];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) lds_publish_step(flag, (uint32_t)t + 1u);  // (W0 clears the emptied tiles)
+      ROLLW_STAMP(9);
+      uint32_t cv = 0;  // the generated berries of the ostrich's tile (:631-635), for W0 (unused
+                        // when W0 clears that tile: it is then in the log with no berries)
+      if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
+        cv = (uint32_t)bush_value_fast(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1),
+                                       p.bush_power);
+      cval[lane] = cv;
+      __builtin_amdgcn_s_setprio(0);
+      ROLLW_STAMP(10);
+      lds_barrier();  // B1
+      ROLLW_STAMP(11);
+      lds_barrier();  // B2
+      ROLLW_STAMP(12);
     } else {
-      if (wave == 1) {
-        // ---------------------------------------------- W1 P0: the view bitmap
-        __builtin_amdgcn_s_setprio(2);
-        // (the view bitmap is scrolled in place in LDS, a few rows at a time: a 32-row register
-        // copy set the whole kernel's register budget, and its spills to scratch are vector
-        // loads that wait for every obs store this wave has in flight)
-        if (t == 0) {
-          const int nthr = p.max_berries;
-          uint64_t tv[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
-          const int64_t ga = active ? g : 0;
-          const uint4* src = reinterpret_cast<const uint4*>(p.bushmap + (size_t)ga * 32u);
-#pragma unroll 1
-          for (int k = 0; k < 8; k += 2) {  // (step 0 only)
-            const uint4 v0 = src[k], v1 = src[k + 1];
-            const uint32_t r[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (4 * k + q < p.W) bm[me + (uint32_t)(4 * k + q)] = r[q];
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
-          if (lane == 0) bush_thr_pads(thr, nthr);
-          __builtin_amdgcn_s_waitcnt(0);
-        } else {  // the last step's eaten-empty tile (its S obs are stored)
-          const unsigned long long jmp = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
-          if (lane < n_active && !((jmp >> lane) & 1ull) && (info[lane] & 2u))
-            bm[me + (uint32_t)p.cw] &= ~(1u << p.ch);
-        }
-        lds_await_step(p, flag + 1, (uint32_t)t + 1u);  // the strip, drawn by W3 meanwhile
-        const uint32_t strip = wstrip[lane];
-        const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
-        const uint32_t top = 1u << (p.H - 1);
-        const int Wv = p.W;
-        uint32_t prev_old = 0u;             // the old row i - 1
-        uint32_t nxt = active ? bm[me] : 0u;  // the old row i
-#pragma unroll 1
-        for (int i0 = 0; i0 < Wv; i0 += 4) {  // scroll (:613-629) + the entering strip, in place
-          uint32_t old[5];
-          old[0] = nxt;
-#pragma unroll
-          for (int q = 1; q < 5; ++q) old[q] = (active && i0 + q < Wv) ? bm[me + (uint32_t)(i0 + q)] : 0u;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int i = i0 + q;
-            if (i >= Wv) break;
-            const uint32_t wi = old[q];
-            const uint32_t prev = q == 0 ? prev_old : old[q - 1];
-            const uint32_t next = old[q + 1];
-            const uint32_t sb = (strip >> i) & 1u;
-            uint32_t v = wi;
-            v = h.dir == DIR_RIGHT ? (i == 0 ? strip : prev) : v;
-            v = h.dir == DIR_LEFT ? (i == Wv - 1 ? strip : next) : v;
-            v = h.dir == DIR_UP ? (((wi << 1) & hmask) | sb) : v;
-            v = h.dir == DIR_DOWN ? ((wi >> 1) | (sb ? top : 0u)) : v;
-            bm[me + (uint32_t)i] = active ? v : 0u;
-          }
-          prev_old = old[3];
-          nxt = old[4];
-        }
+      // ---------------------------------------------- W3: the strip for W1; W2: tables, spawn set;
+      // then both store the last step's obs
+      if (wave == 3) {  // the entering strip's draws, for W1's scroll
+        wstrip[lane] = active ? strip_bits(p, h) : 0u;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) lds_publish_step(flag, (uint32_t)t + 1u);  // (W0 clears the emptied tiles)
-        ROLLW_STAMP(9);
-        uint32_t cv = 0;  // the generated berries of the ostrich's tile (:631-635), for W0 (unused
-                          // when W0 clears that tile: it is then in the log with no berries)
-        if (active && ((bm[me + (uint32_t)p.cw] >> p.ch) & 1u))
-          cv = (uint32_t)bush_value_fast(thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), h.b0, h.b1),
-                                         p.bush_power);
-        cval[lane] = cv;
-        __builtin_amdgcn_s_setprio(0);
-        ROLLW_STAMP(10);
+        if (lane == 0) lds_publish_step(flag + 1, (uint32_t)t + 1u);
       } else {
-        // ---------------------------------------------- W3: ostrich grids; W2: tables, spawn set
-        if (wave == 3) {  // the entering strip's draws, for W1's scroll
-          wstrip[lane] = active ? strip_bits(p, h) : 0u;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_wave_barrier();
-          if (lane == 0) lds_publish_step(flag + 1, (uint32_t)t + 1u);
+        if (t == 0) {
+          copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
+          if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
+          __builtin_amdgcn_s_waitcnt(0);
         }
-        if (wave == 2) {
-          if (t == 0) {
-            copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
-            if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
-            __builtin_amdgcn_s_waitcnt(0);
-          }
-          for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_wave_barrier();
-          if (p.wolves_on && active)
-            spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
-              spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
-            });
-          ROLLW_STAMP(17);
-        }
+        for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (p.wolves_on && active)
+          spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
+            spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
+          });
       }
+      ROLLW_STAMP(8 * wave + 1);
+      RowCursor rc = row_cursor(p, (uint32_t)(tid - 128));  // (thread tid - 128 of the two store waves)
+      if (t > 0)  // step t - 1's rows until W0 reaches B1 (two rows per check)
+        while (rc.q < n_rows && !lds_reached(flag + 2, at_b1)) {
+          roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+          if (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+        }
+      ROLLW_STAMP(8 * wave + 2);
       lds_barrier();  // B1
-      ROLLW_STAMP(8 * wave + (wave == 1 ? 3 : 2));
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
+      if (t > 0)  // ... until W0 reaches B2
+        while (rc.q < n_rows && !lds_reached(flag + 2, at_b2)) {
+          roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+          if (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+        }
+      ROLLW_STAMP(8 * wave + 3);
       lds_barrier();  // B2
-      ROLLW_STAMP(8 * wave + (wave == 1 ? 4 : 3));
-      obs_rows(p, bm, wp, out, (uint32_t)n_active, ((unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32)),
-               false, tid);
-      ROLLW_STAMP(8 * wave + (wave == 1 ? 5 : 4));
+      if (t > 0)  // ... and the rest, while W0 and W1 build the new episodes
+        while (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+      ROLLW_STAMP(8 * wave + 4);
     }
 
-    if (wave == 0) ROLLW_STAMP(7);
     const int n_jobs = (int)blk[0];
     const unsigned long long jmask = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
-    // ------------------------------------------------ P2: the continuing envs' bitmaps (post-eat)
-    // (the continuing envs' eaten-empty tiles are cleared from bm by W1 at the next step's start)
     if (wave == 0) {
       if (eaten_of) atomicAdd(&p.counters[CTR_EATEN_OVERFLOW], eaten_of);
       if (lane == 0 && n_jobs) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)n_jobs);
       count_steps(p);
     }
-    if (n_jobs > 0) {
-      // ------------------------------------------------ done envs: new episodes (:231-248)
-      lds_barrier();  // B3: the eaten-empty clears are in (a job's rows are redrawn below)
+    if (n_jobs > 0 && wave < 2) {
+      // ------------------------------------------------ done envs: new episodes (:231-248), by W0
+      // and W1 (the store waves keep storing): reset draws (generate_bushes) over the new view,
+      // ostrich at (0, 0), 32 lanes per row, rows written by ballot into this step's bitmaps;
+      // initialize_wolves (:578-593): the view's spawn set at turn 0, by the job's own lane of W0
       const uint32_t ts_bush = make_ts(SITE_BUSH, 0, 0);
       const uint32_t rows2 = ((uint32_t)p.W + 1u) >> 1;
       for (int jj = 0; jj < n_jobs; ++jj) {
         const uint32_t e = jobEnv[jj];
         const uint2 kq = *reinterpret_cast<const uint2*>(&jobKey[2 * jj]);
-        for (uint32_t r2 = (uint32_t)wave; r2 < rows2; r2 += 4u) {
+        for (uint32_t r2 = (uint32_t)wave; r2 < rows2; r2 += 2u) {
           const uint32_t i = 2u * r2 + ((uint32_t)lane >> 5), j = (uint32_t)lane & 31u;
           const bool cell = i < (uint32_t)p.W && j < (uint32_t)p.H;
           const uint32_t xy = xy_pack(p.cw - (int)i, p.ch - (int)j);
@@ -1487,21 +1512,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         }
       }
       if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
-        const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
-        for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;
-        if (p.wolves_on)
-          spawn_hits(gap, p.WH, p.gap_full_th, p.gap_full_tl, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, (uint32_t)ek2,
-                     (uint32_t)(ek2 >> 32), [&](int c) {
-                       const uint32_t i = (uint32_t)c / (uint32_t)p.H;
-                       wp[me + i] |= 1u << ((uint32_t)c - i * (uint32_t)p.H);
-                     });
-      }
-      lds_barrier();  // B4
-      if (wave == 0) ROLLW_STAMP(37);
-      if (wave == 0 && active && ((jmask >> lane) & 1ull)) {
         // spawn_ostriches (:595-611) and the initial wolves, one per wolf cell of the view
         const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));
         const uint32_t kb0 = (uint32_t)ek2, kb1 = (uint32_t)(ek2 >> 32);
+        for (int i = 0; i < p.W; ++i) wp[me + (uint32_t)i] = 0u;
+        if (p.wolves_on)
+          spawn_hits(gap, p.WH, p.gap_full_th, p.gap_full_tl, p.gap_view_th, p.gap_view_tl, p.gap_inv_l2, 0, kb0, kb1,
+                     [&](int c) {
+                       const uint32_t i = (uint32_t)c / (uint32_t)p.H;
+                       wp[me + i] |= 1u << ((uint32_t)c - i * (uint32_t)p.H);
+                     });
         const double food2 = p.start_food_random
                                  ? (double)draw_U(xy_pack(0, 0), make_ts(SITE_START_FOOD, 0, 0), kb0, kb1) * 0x1p-53
                                  : p.start_food;
@@ -1547,13 +1567,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food2;
         }
       }
-      // the lines that touch a done env: its new episode, its neighbours' S
-      obs_rows(p, bm, wp, out, (uint32_t)n_active, jmask, true, tid);
     }
     if (wave == 0) ROLLW_STAMP(39);
     if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
-    if (last) {  // every env's bitmap rows (continuing: post-eat; done: the new episode's)
-      lds_barrier();
+    lds_barrier();  // the step's end: its obs buffers are complete; the next step's inputs are in
+    if (last) {
+      // the last step's obs, by all 256 threads; every env's bitmap rows (continuing: post-eat;
+      // done: the new episode's)
+      RowCursor c = row_cursor(p, (uint32_t)tid);
+      while (c.q < n_rows) roll_store_row<256>(p, bm, wp, out, c);
       for (uint32_t u = tid; u < 64u * 32u; u += 256) {
         const uint32_t e = u >> 5, i = u & 31u;
         if ((int)e >= n_active || i >= (uint32_t)p.W) continue;
@@ -1562,7 +1584,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         p.bushmap[(size_t)(g0 + e) * 32u + i] = v;
       }
     }
-    lds_barrier();  // the step's end: its LDS (bm, wp, nhdr, act) is the next step's input
   }
 }
 
