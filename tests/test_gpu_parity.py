@@ -1011,3 +1011,28 @@ def test_env_buffers_after_rollouts():
     e1.step(a[0])
     e2.step(a[0])
     assert torch.equal(w1.observation(), w2.observation())
+
+
+def test_rollout_features_ambiguous_rewards_fail_before_stepping():
+    """Options whose step rewards collide in float32 (r_x and r_eat + r_x) cannot give exact
+    returns from the scan kernel: a rollout_features call that would need it (T > 128) fails
+    before any step runs (the env's counters do not move); T <= 128 fuses the returns from the
+    reward codes and works; returns=False always works."""
+    import torch
+
+    from wab_gym_amd.options import default_game_options
+
+    o = dict(default_game_options)
+    o["reward_for_eating"] = 1e-12
+    o["reward_per_turn"] = 0.3
+    env = _env(o, 256, validate_actions=False)
+    env.reset()
+    a = torch.zeros((130, 256), dtype=torch.int8, device="cuda:0")
+    steps0 = env.counters()["steps"]
+    with pytest.raises(ValueError):
+        env.rollout_features(a)
+    assert env.counters()["steps"] == steps0
+    r = env.rollout_features(a[:64])
+    assert r["returns"] is not None
+    r = env.rollout_features(a, returns=False)
+    assert r["returns"] is None and env.counters()["steps"] == steps0 + 194 * 256

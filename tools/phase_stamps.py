@@ -303,10 +303,14 @@ def rollout_report(env, st, g, launches, T, features=False):
             ok = (v > 0).all(axis=1)
             acc[k].append((v[ok] - t0[ok, None]).mean(axis=0))
         spans.append((s[:, [5, 14, 20, 26]].max(axis=1) - t0).mean())
+        acc.setdefault("loop", []).append(((s[:, 0] - s[:, 35]).mean(), (s[:, 38] - t0).mean()))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
     print("step start -> last wave past B2 (mean over workgroups): %.2f us" % (np.mean(spans) * 10 / 1000))
+    lp = np.mean(acc["loop"], axis=0) * 10 / 1000
+    print("W0: loop top -> its start (parameters, slices) %.2f us; step start -> past its end barrier %.2f us"
+          % (lp[0], lp[1]))
     if features:
         f = np.mean(acc["feat"], axis=0) * 10 / 1000
         print("features: emitted %.2f, wave 0's row stores issued %.2f us" % (f[0], f[1]))

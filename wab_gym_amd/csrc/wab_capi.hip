@@ -896,8 +896,20 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
   if (obs_seq->planes && (!aligned16(obs_seq->planes) || (T > 1 && ((size_t)B * OB) % 16u != 0)))
     return fail(WAB_E_INVALID, "wab_rollout_features: every step's planes must be 16-byte aligned");
   if (T == 0 || B == 0) return WAB_OK;
-  const bool fused_returns = returns && T <= wab::kMaxFusedReturnSteps;
+  bool fused_returns = returns && T <= wab::kMaxFusedReturnSteps;
+  size_t roll_lds = 0;  // the fused launch's LDS (its reward codes grow with T)
   if (h->small_feat_lds_bytes && h->step_kernel == KERNEL_SMALL) {
+    Params q = h->p;
+    q.features = features;
+    q.n_steps = T;
+    q.returns = fused_returns ? returns : nullptr;
+    roll_lds = (size_t)wab::small_layout(q).total * 4u;
+    if (roll_lds > 64u * 1024u) roll_lds = 0;  // (T steps of the per-step fused launch instead)
+  }
+  if (returns && !(roll_lds && fused_returns) && h->rewards.n < 0)  // (checked before anything runs)
+    return fail(WAB_E_INVALID, "wab_rollout_features: returns of this segment need the exact-reward scan, and "
+                               "two of the options' rewards round to the same float32 (pass returns = NULL)");
+  if (roll_lds) {
     // one launch: each workgroup runs its 64 envs through the T steps with the featurizer fused
     // (wab_step_small<.., FEAT, ROLL>), the returns of the segment at its end
     Params p = h->p;
@@ -915,10 +927,9 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
       p.bootstrap = bootstrap;
       p.gamma = gamma;
     }
-    const size_t lds = (size_t)wab::small_layout(p).total * 4u;
     DeviceGuard guard(h->device);
-    if (h->small_g11) launch_small<11, true, true>(h, p, (hipStream_t)stream, lds);
-    else launch_small<0, true, true>(h, p, (hipStream_t)stream, lds);
+    if (h->small_g11) launch_small<11, true, true>(h, p, (hipStream_t)stream, roll_lds);
+    else launch_small<0, true, true>(h, p, (hipStream_t)stream, roll_lds);
     HIP_TRY(hipGetLastError());
     if (fused_returns) return WAB_OK;
   } else {

@@ -1481,6 +1481,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     // depend on nothing outside it), each wave's state carried in registers from step to step
     // (see CarryW0): one barrier closes a step (its LDS is reused by the next)
     const int T = p0.n_steps;
+#ifdef WAB_STAMPS
+#define ROLL_LOOP_STAMP(slot, cond)                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && p0.stamps && (cond))                                             \
+      p0.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+#else
+#define ROLL_LOOP_STAMP(slot, cond) do {} while (0)
+#endif
     {  // the second stream starts clear (the first is cleared by W0 in step 0)
       const SmallLayout L = small_layout(p0);
       uint4* z = reinterpret_cast<uint4*>(lds + L.stream2);
@@ -1490,6 +1499,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     // t - 1's obs from the other one; the last step's obs go out at its end, by every thread
 #define WAB_ROLL_STEP(...)                                                                   \
     for (int t = 0; t < T; ++t) {                                                            \
+      ROLL_LOOP_STAMP(35, t == T / 2);  /* the middle step's loop top (before its parameters) */ \
       Params p = wave_params<G, FEAT>(p0);                                                   \
       step_slice(p, t);                                                                      \
       const SmallLayout L0 = small_layout(p);                                                \
@@ -1509,6 +1519,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
         store_units_of<0, 6>(p, lds + L.stream, threadIdx.x);                                \
       }                                                                                      \
       lds_barrier();                                                                         \
+      ROLL_LOOP_STAMP(38, t == T / 2);  /* past the middle step's end barrier */             \
     }
     if (wave == 0) {
       CarryW0 c;
@@ -1528,6 +1539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
       WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1)))
     }
 #undef WAB_ROLL_STEP
+#undef ROLL_LOOP_STAMP
   }
 }
 
