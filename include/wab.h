@@ -179,7 +179,9 @@ int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* re
  * or the wide kernel steps the handle (wab_step_kernel "small" / "wide") and B * width *
  * plane_stride * 3 is a multiple of 16, this is ONE launch: each workgroup takes its 64 envs
  * through the T steps with their state on chip (loaded by the first step, stored by the
- * last); otherwise T wab_step launches. */
+ * last); otherwise T wab_step launches (a step slice that is not 16-byte aligned goes through
+ * a handle-owned [B] buffer, allocated synchronously by the first such call, and a
+ * device-to-device copy on `stream`). */
 int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq,
                 float* reward, uint8_t* done, void* stream);
 
@@ -237,8 +239,10 @@ int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, 
  * fused small-view kernel steps the handle this is ONE launch: every workgroup takes its 64 envs
  * through the T steps with the state in registers, step t's feature rows stored while step
  * t + 1 runs, and (T <= 128) the returns computed from each step's exact double reward at the
- * end; elsewhere T wab_step_features calls and wab_discounted_returns_exact.  Every step's
- * features (and planes, if set) must be 16-byte aligned: B * F (B * OB) a multiple of 4 (16). */
+ * end; elsewhere T wab_step_features calls and wab_discounted_returns_exact (misaligned plane
+ * slices as in wab_rollout).  Every step's features must be 16-byte aligned: B * F a multiple
+ * of 4.  With returns, T > 128 (or a non-fused handle) needs the exact-reward scan: when two of
+ * the options' rewards round to the same float32 the call fails before any step runs. */
 int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* obs_seq,
                          float* reward, uint8_t* done, float* features, double gamma,
                          const float* bootstrap, float* returns, void* stream);

@@ -299,6 +299,19 @@ int launch_returns(const float* reward, const uint8_t* done, int32_t T, int64_t 
   return WAB_OK;
 }
 
+// a handle-owned [B] obs planes buffer (16-byte aligned), allocated by the first call that needs it
+uint8_t* scratch_planes(wab_handle* h) {
+  if (!h->scratch_planes) {
+    DeviceGuard guard(h->device);
+    void* ptr = nullptr;
+    const size_t bytes = std::max<size_t>(16, (size_t)h->p.B * (size_t)h->p.OB);
+    if (hipMalloc(&ptr, bytes) != hipSuccess) return nullptr;
+    h->allocs.push_back(ptr);
+    h->scratch_planes = static_cast<uint8_t*>(ptr);
+  }
+  return h->scratch_planes;
+}
+
 int check_obs(const wab_obs* o, const char* what) {
   if (!o || !o->planes || !o->food_turns || !o->role || !o->status)
     return fail(WAB_E_INVALID, std::string(what) + ": every wab_obs pointer must be set");
@@ -711,13 +724,21 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
   }
   for (int32_t t = 0; t < T; ++t) {
     wab_obs o;
-    o.planes = obs_seq->planes + (size_t)t * (size_t)B * OB;
+    uint8_t* dst = obs_seq->planes + (size_t)t * (size_t)B * OB;
+    // (a step slice that is not 16-byte aligned, B * OB % 16 != 0: the step writes a handle-owned
+    // buffer, copied to the slice on the stream; the first such call allocates it)
+    o.planes = aligned16(dst) ? dst : scratch_planes(h);
+    if (!o.planes) return fail(WAB_E_NOMEM, "wab_rollout: hipMalloc");
     o.food_turns = obs_seq->food_turns + (size_t)t * (size_t)B;
     o.role = obs_seq->role + (size_t)t * (size_t)B;
     o.status = obs_seq->status + (size_t)t * (size_t)B;
     int rc = wab_step(h, actions + (size_t)t * (size_t)B, &o, reward + (size_t)t * (size_t)B,
                       done + (size_t)t * (size_t)B, nullptr, stream);
     if (rc != WAB_OK) return rc;
+    if (o.planes != dst) {
+      DeviceGuard guard(h->device);
+      HIP_TRY(hipMemcpyAsync(dst, o.planes, (size_t)B * OB, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    }
   }
   return WAB_OK;
 }
@@ -846,15 +867,8 @@ int wab_step_features(wab_handle* h, const int8_t* actions, const wab_obs* obs, 
     // (without caller planes through a handle-owned buffer, allocated by the first such call)
     wab_obs o = *obs;
     if (!o.planes) {
-      if (!h->scratch_planes) {
-        DeviceGuard guard(h->device);
-        void* ptr = nullptr;
-        const size_t bytes = std::max<size_t>(16, (size_t)h->p.B * (size_t)h->p.OB);
-        if (hipMalloc(&ptr, bytes) != hipSuccess) return fail(WAB_E_NOMEM, "wab_step_features: hipMalloc");
-        h->allocs.push_back(ptr);
-        h->scratch_planes = static_cast<uint8_t*>(ptr);
-      }
-      o.planes = h->scratch_planes;
+      o.planes = scratch_planes(h);
+      if (!o.planes) return fail(WAB_E_NOMEM, "wab_step_features: hipMalloc");
     }
     if (int rc = wab_step(h, actions, &o, reward, done, nullptr, stream)) return rc;
     return wab_featurize(h, &o, nullptr, features, stream);
@@ -893,8 +907,8 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
   if (!aligned16(features) || (T > 1 && ((size_t)B * (size_t)F * 4u) % 16u != 0))
     return fail(WAB_E_INVALID, "wab_rollout_features: every step's features must be 16-byte aligned "
                                "(features aligned, batch * feature_dim a multiple of 4)");
-  if (obs_seq->planes && (!aligned16(obs_seq->planes) || (T > 1 && ((size_t)B * OB) % 16u != 0)))
-    return fail(WAB_E_INVALID, "wab_rollout_features: every step's planes must be 16-byte aligned");
+  if (obs_seq->planes && !aligned16(obs_seq->planes))
+    return fail(WAB_E_INVALID, "wab_rollout_features: planes must be 16-byte aligned");
   if (T == 0 || B == 0) return WAB_OK;
   bool fused_returns = returns && T <= wab::kMaxFusedReturnSteps;
   size_t roll_lds = 0;  // the fused launch's LDS (its reward codes grow with T)
@@ -905,6 +919,7 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
     q.returns = fused_returns ? returns : nullptr;
     roll_lds = (size_t)wab::small_layout(q).total * 4u;
     if (roll_lds > 64u * 1024u) roll_lds = 0;  // (T steps of the per-step fused launch instead)
+    if (obs_seq->planes && ((size_t)B * OB) % 16u != 0) roll_lds = 0;  // (its 16-byte obs stores)
   }
   if (returns && !(roll_lds && fused_returns) && h->rewards.n < 0)  // (checked before anything runs)
     return fail(WAB_E_INVALID, "wab_rollout_features: returns of this segment need the exact-reward scan, and "
@@ -936,6 +951,11 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
     for (int32_t t = 0; t < T; ++t) {  // (no fused kernel for these options: T fused-or-not steps)
       wab_obs o;
       o.planes = obs_seq->planes ? obs_seq->planes + (size_t)t * (size_t)B * OB : nullptr;
+      uint8_t* dst = o.planes;
+      if (dst && !aligned16(dst)) {  // (as in wab_rollout: through the handle's buffer)
+        o.planes = scratch_planes(h);
+        if (!o.planes) return fail(WAB_E_NOMEM, "wab_rollout_features: hipMalloc");
+      }
       o.food_turns = obs_seq->food_turns + (size_t)t * (size_t)B;
       o.role = obs_seq->role + (size_t)t * (size_t)B;
       o.status = obs_seq->status + (size_t)t * (size_t)B;
@@ -943,6 +963,10 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
                                  done + (size_t)t * (size_t)B, features + (size_t)t * (size_t)B * (size_t)F,
                                  stream);
       if (rc != WAB_OK) return rc;
+      if (dst && o.planes != dst) {
+        DeviceGuard guard(h->device);
+        HIP_TRY(hipMemcpyAsync(dst, o.planes, (size_t)B * OB, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      }
     }
   }
   if (!returns) return WAB_OK;
