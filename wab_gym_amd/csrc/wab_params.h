@@ -161,11 +161,8 @@ constexpr int kMaxFusedReturnSteps = 128;
 struct SmallLayout {
   uint32_t tiles, thr, gap, stream, stream_words, cval, flag, wolfp, kill, bushp, strip, gone, info, spawn, jbm, jkey;
   uint32_t carry, act;  // multi-step launches: the new episodes' state for the next step, its actions
-  uint32_t sync;        // multi-step launches: [0], [1] store-pool claims (by step parity), [2] barrier arrivals
   uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
-  uint32_t fwords;      // ... the feature bits' region (dwords)
-  uint32_t fbits2;      // multi-step fused features: the odd steps' feature bits (rows stored a step later)
   uint32_t rcode;       // wab_rollout_features with returns: [n_steps][64] reward codes (bytes)
 };
 
@@ -190,23 +187,18 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.jkey = o; o += 2u * 2u * 64u;
   L.carry = o; o += 8u * 64u;  // per env: role | new wolves << 8, food (2), wolf cells (4), pad
   L.act = o; o += 16u;         // 64 int8 actions
-  L.sync = o; o += 4u;
   L.stream2 = o; o += L.stream_words + 4u;
   L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
-  L.fbits = L.ftab = L.fzero = L.scal = L.fbits2 = o;
-  L.fwords = 0;
+  L.fbits = L.ftab = L.fzero = L.scal = o;
   if (p.features) {  // fused features: 64 envs x F bits (+ slack), the per-cell tables (zeroed
-                     // together), the envs' scalars; multi-step launches a second bits buffer
+                     // together), the envs' scalars
     const int md = p.W / 2 + p.H / 2 + 1;
     const uint32_t F = (uint32_t)(16 * (md + 1) + 88 + 2 + (p.turns_empty + 1) + 2 + 3 + 121);
-    L.fwords = lds_align4(((64u * F + 31u) >> 5) + 4u);
-    L.fbits = o; o += L.fwords;
+    L.fbits = o; o += lds_align4(((64u * F + 31u) >> 5) + 4u);
     L.ftab = o; o += lds_align4(128u + 4u * ((uint32_t)md + 4u));
     L.fzero = o - L.fbits;
     L.scal = o; o += 64u;
-    L.fbits2 = o;
-    if (p.n_steps > 1) o += L.fwords;
   }
   L.rcode = o;
   if (p.returns) o += 16u * (uint32_t)p.n_steps;  // one byte per env and step

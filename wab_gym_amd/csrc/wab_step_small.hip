@@ -372,114 +372,45 @@ __device__ __forceinline__ void render_s(const Params& p, const Lds& s, int lane
 // while W3 builds the new episodes: 10.34 -> 12.02 us at B = 65536, the stores of all groups
 // then share the HBM while W0-W2 still have to reach B2.)
 
-// --------------------------------------------------------------------------- multi-step launches: the store pool
-// A multi-step launch stores step t's outputs during step t + 1: its obs (the stream of step t
-// & 1; each unit cleared after its read so that step t + 2 can render into it again) and, with
-// the fused featurizer, its feature rows (from the feature bits of step t & 1).  The stores are
-// a pool of items, one wave-instruction each (64 obs units of 16 bytes, or 64 float4s of the
-// rows: 1 KiB, eight whole 128-byte lines), claimed one at a time by whichever wave is waiting
-// at a barrier of step t + 1 while the others have not arrived (roll_barrier), and drained by
-// every wave at the step's end barrier.  So the stores fill the waves' waits instead of holding
-// a barrier: no barrier waits for more than one item's issue, and the store stream of a
-// workgroup runs through its whole step.
-struct RollPool {
-  uint32_t* claims;      // this step's claim counter (Lds sync[t & 1])
-  uint32_t* arrive;      // arrivals at pool barriers (sync[2], monotonic)
-  uint32_t n_obs, n_items;
-  uint8_t* planes;       // step t - 1's obs slice (null: the units are only cleared)
-  uint16_t* s16;         // step t - 1's stream
-  uint32_t full;         // its 16-byte units
-  const uint32_t* fbits; // step t - 1's feature bits (null: no features)
-  float* feats;          // the group's rows of step t - 1
-  uint32_t nq, nf;       // float4s, floats of the group's rows
-};
-
-// the pool of step t (the outputs of step t - 1); empty at t = 0
-__device__ __forceinline__ RollPool roll_pool(const Params& p, uint32_t* lds, int t) {
-  const SmallLayout L0 = small_layout(p);  // (unswapped: stream / fbits are the even steps')
-  RollPool q;
+// Multi-step launches (wab_rollout): NT threads (index idx) store NK units each (u = idx + NT
+// * k) of a finished step's stream into `planes` (that step's slice), non-temporal, clearing
+// each unit after its read so the stream can be rendered into again.  (Measured and not
+// adopted: the store instructions aligned to absolute 128-byte lines, plain stores, the units
+// in smaller read/clear/store batches; the obs stores split over W0, W2 and W3.)
+template <int NT, int NK>
+__device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes, uint32_t* stream, int idx) {
   const int64_t g0 = (int64_t)blockIdx.x * 64;
-  const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
-  q.claims = lds + L0.sync + (uint32_t)(t & 1);
-  q.arrive = lds + L0.sync + 2u;
-  q.planes = p.planes ? p.planes - (int64_t)p.B * p.OB + (size_t)g0 * (uint32_t)p.OB : nullptr;
-  q.s16 = reinterpret_cast<uint16_t*>(lds + ((t & 1) ? L0.stream : L0.stream2));
-  q.full = (n_active * (uint32_t)p.OB) >> 4;
-  q.n_obs = t > 0 ? (q.full + 63u) >> 6 : 0u;
-  q.fbits = nullptr;
-  q.feats = nullptr;
-  q.nq = q.nf = 0u;
-  uint32_t n_feat = 0;
-  if (p.features && t > 0) {
-    const uint32_t F = (uint32_t)pragmatic_dim(p.W / 2 + p.H / 2 + 1, p.turns_empty);
-    q.fbits = lds + ((t & 1) ? L0.fbits : L0.fbits2);
-    q.feats = p.features - (int64_t)p.B * F + (size_t)g0 * F;
-    q.nf = n_active * F;
-    q.nq = q.nf >> 2;
-    n_feat = (q.nq + 63u) >> 6;
-    if (q.nf & 3u) n_feat = max(n_feat, (q.nq >> 6) + 1u);  // (the float tail rides on the last item)
-  }
-  q.n_items = q.n_obs + n_feat;
-  return q;
-}
-
-// claim and store one item of the pool; false when it is empty
-__device__ __forceinline__ bool pool_store_one(const RollPool& q, int lane) {
-  uint32_t i = 0;
-  if (lane == 0) i = atomicAdd(q.claims, 1u);
-  i = (uint32_t)__shfl((int)i, 0);
-  if (i >= q.n_items) return false;
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  if (i < q.n_obs) {
-    const uint32_t u = 64u * i + (uint32_t)lane;
-    if (u < q.full) {
-      const uint32_t v = q.s16[u];
-      q.s16[u] = 0;
-      if (q.planes) {
-        u32x4 w;
+  const uint32_t OB = (uint32_t)p.OB;
+  const uint32_t full = ((uint32_t)min((int64_t)64, p.B - g0) * OB) >> 4;
+  uint8_t* out = planes + (size_t)g0 * OB;
+  uint16_t* s16 = reinterpret_cast<uint16_t*>(stream);
+  uint32_t v[NK];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) w[b] = (((v >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(q.planes) + u);
-      }
-    }
-  } else {
-    const uint32_t j = i - q.n_obs, u = 64u * j + (uint32_t)lane;
-    if (u < q.nq) {
-      const uint32_t w = q.fbits[u >> 3], sh = 4u * (u & 7u);
-      float4 f;
-      f.x = (float)__builtin_amdgcn_ubfe(w, sh, 1u);
-      f.y = (float)__builtin_amdgcn_ubfe(w, sh + 1u, 1u);
-      f.z = (float)__builtin_amdgcn_ubfe(w, sh + 2u, 1u);
-      f.w = (float)__builtin_amdgcn_ubfe(w, sh + 3u, 1u);
-      nt_store_f4(f, reinterpret_cast<float4*>(q.feats) + u);
-    }
-    const uint32_t tq = 4u * q.nq + (uint32_t)lane;  // the group's last floats (nf % 4), last item
-    if (j == q.n_items - q.n_obs - 1u && tq < q.nf)
-      q.feats[tq] = ((q.fbits[tq >> 5] >> (tq & 31u)) & 1u) ? 1.0f : 0.0f;
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)(idx + NT * k);
+    v[k] = u < full ? (uint32_t)s16[u] : 0u;
   }
-  return true;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)(idx + NT * k);
+    if (u < full) s16[u] = 0;
+  }
+  if (!planes) return;  // (wab_rollout_features without planes: the stream is only cleared)
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const uint32_t u = (uint32_t)(idx + NT * k);
+    if (u >= full) continue;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 q;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+  }
 }
 
-// barrier k of a multi-step launch's step (counted over the launch: every wave passes the same
-// sequence): a wave that arrives before the others stores pool items until they are all in
-// (drain: until the pool is empty), then the barrier
-__device__ __forceinline__ void roll_barrier(const RollPool& q, uint32_t k, int lane, bool drain = false) {
-  if (lane == 0) atomicAdd(q.arrive, 1u);
-  while (true) {
-    if (!drain) {
-      const uint32_t a = (uint32_t)__shfl((int)__hip_atomic_load(q.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
-      if (a >= 4u * k) break;
-    }
-    if (!pool_store_one(q, lane)) break;
-  }
-  lds_barrier();
-}
-// pool barriers per step: B1, B2 and the step's end
-constexpr uint32_t kRollBarriers = 3;
-__device__ __forceinline__ uint32_t roll_barrier_index(int t, uint32_t j) { return kRollBarriers * (uint32_t)t + j; }
-
-// Diagnostic build -DWAB_ROLL_FLOOR=1: every step's work skipped, its obs stores kept (the store
-// pattern's own floor; results wrong by design)
+// Multi-step launches store step t's obs during step t + 1 (streams alternate), by W0 and W2 in
+// their slack before B2 (W1 and W3 never store).  Diagnostic build -DWAB_ROLL_FLOOR=1: every
+// step's work skipped, its obs stores kept (the store pattern's own floor; results wrong by design)
 #ifndef WAB_ROLL_FLOOR
 #define WAB_ROLL_FLOOR 0
 #endif
@@ -496,6 +427,8 @@ struct CarryHdr {
   uint4 hdr;  // the env's header at the start of the next step, as far as this wave uses it
 };
 struct CarryW0 {
+  uint8_t* prev_planes;   // the previous step's obs slice and stream, or null
+  uint32_t* prev_stream;
   uint4 hdr;
   double food;
   uint32_t bw[4];            // view bitmap (post-eat)
@@ -503,9 +436,18 @@ struct CarryW0 {
 };
 template <int SLOTS>
 struct CarryW2 {
+  uint8_t* prev_planes;
+  uint32_t* prev_stream;
   uint4 hdr;
   uint32_t wr[SLOTS];  // wolf tiles, uncompacted
   uint32_t live;       // occupied slots
+};
+
+template <typename C>
+struct CarryPtr {  // (W1, W3: the loop's previous-step fields, unused by these waves)
+  uint8_t* prev_planes;
+  uint32_t* prev_stream;
+  C c;
 };
 
 __device__ __forceinline__ int act_of(const Lds& s, int lane) {
@@ -834,8 +776,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   if (starved) food = 0.0;
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
   SMALL_STAMP(3);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 1), lane);  // B1
-  else lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
+  lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
   __builtin_amdgcn_s_setprio(1);
 
   // status (starve overrides kill), reward/done (:328-340), scalars, bushes and food
@@ -881,9 +822,9 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   count_steps(p);
   const unsigned long long jm = __ballot(job);
   if (lane == 0 && jm) atomicAdd(&p.block_resets[blockIdx.x], (unsigned long long)__popcll(jm));  // (no-return: a load here would wait for the stores)
+  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
   SMALL_STAMP(4);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 2), lane);  // B2
-  else lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
+  lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
   if (p.t_planes) {
     // terminal obs: the step's own obs of every done env (bytes); then its new episode
     unsigned long long wolf_of = 0;
@@ -993,8 +934,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   SMALL_STAMP(11);
   s.strip[lane] = strip_draws(p, h, b0, b1, 0, kStripW1);  // generate_bushes (:613-629): the entering strip
   SMALL_STAMP(12);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 1), lane);  // B1
-  else lds_barrier();  // B1
+  lds_barrier();  // B1
   const uint32_t info = s.info[lane];
   const bool killed = s.kill[lane] != 0u;
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), killed);
@@ -1021,8 +961,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     render_s(p, s, lane, info, h.dir);
   }
   SMALL_STAMP(13);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 2), lane);  // B2
-  else lds_barrier();  // B2
+  lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(14);
   if (ROLL && lane == 0) {  // every hand-off of this step is done: clear the flags for the next
@@ -1149,8 +1088,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   s.kill[lane] = kill ? 1u : 0u;
   SMALL_STAMP(17);
   SMALL_STAMP(18);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 1), lane);  // B1
-  else lds_barrier();  // B1: the spawn set, the starve flags and the bushes' counts are in
+  lds_barrier();  // B1: the spawn set, the starve flags and the bushes' counts are in
   const uint32_t info = s.info[lane];
   const bool starved = info_starved(info);
   const bool job = active && p.autoreset && env_done(p, h, starved, kill);
@@ -1189,9 +1127,9 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   }
   if (wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
   const unsigned long long jm = __ballot(job);
+  if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
   SMALL_STAMP(19);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 2), lane);  // B2
-  else lds_barrier();  // B2
+  lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(20);
   if (ROLL && !last) {  // the slots for the next step: a new episode's wolves from W3's cells
@@ -1264,7 +1202,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   if (p.features) {  // zero the fused features' bits and tables (contiguous, 16-byte aligned;
                      // multi-step launches: the tables once, the bits every step)
     uint4* z = reinterpret_cast<uint4*>(lds + L.fbits);
-    const uint32_t nz = ROLL && t > 0 ? L.fwords : L.fzero;
+    const uint32_t nz = ROLL && t > 0 ? L.ftab - L.fbits : L.fzero;
     for (uint32_t i = lane; i < nz / 4u; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const Head h = head_decode(p, g, g < p.B, hr);
@@ -1284,8 +1222,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   s.spawn[lane] = m_pack(spawn);
   s.strip[64 + lane] = strip_draws(p, h, b0, b1, kStripW1, 1 << 30);  // the entering strip, part 2
   SMALL_STAMP(23);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 1), lane);  // B1
-  else lds_barrier();  // B1
+  lds_barrier();  // B1
   __builtin_amdgcn_s_setprio(3);
   // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
   // (unless the terminal obs is asked for: W0 after B2) the new episodes themselves
@@ -1316,8 +1253,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
     }
   }
   SMALL_STAMP(25);
-  if (ROLL) roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 2), lane);  // B2
-  else lds_barrier();  // B2
+  lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(26);
   if (ROLL && !last) {
@@ -1446,10 +1382,9 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   };
   stamp(36);  // the feature bits emitted
 #endif
-  // Multi-step launches: the rows of step t go out during step t + 1 through the store pool
-  // (double-buffered feature bits), the last step's right here; non-temporal.  (Measured and not
-  // adopted there: the view-mask zero lines stored early in each step.)
-  if (ROLL && t != p.n_steps - 1) return;
+  // (Measured and not adopted in multi-step launches: the rows of step t stored during step t + 1
+  // by W0 and W2 in their slack, from double-buffered feature bits; the view-mask zero lines
+  // stored early in each step.)  Multi-step launches store the rows non-temporal.
   lds_barrier();
   constexpr bool NT = ROLL;
   if (p.restrict_view || ROLL) store_feature_bits<NT>(ob, p.features + (size_t)g0 * F, n_active * F, (int)threadIdx.x, 256);
@@ -1555,12 +1490,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
 #else
 #define ROLL_LOOP_STAMP(slot, cond) do {} while (0)
 #endif
-    {  // the second stream starts clear (the first is cleared by W0 in step 0), the pool's
-       // counters at zero (step 0's B_init orders both)
+    {  // the second stream starts clear (the first is cleared by W0 in step 0)
       const SmallLayout L = small_layout(p0);
       uint4* z = reinterpret_cast<uint4*>(lds + L.stream2);
       for (uint32_t i = threadIdx.x; i < L.stream_words / 4u; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
-      if (threadIdx.x < 4) lds[L.sync + threadIdx.x] = 0u;
     }
     // one step of wave W's part; step t renders into stream t & 1 while W0 and W2 store step
     // t - 1's obs from the other one; the last step's obs go out at its end, by every thread
@@ -1571,23 +1504,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
       step_slice(p, t);                                                                      \
       const SmallLayout L0 = small_layout(p);                                                \
       SmallLayout L = L0;                                                                    \
-      if (t & 1) {                                                                           \
-        L.stream = L0.stream2;                                                               \
-        L.fbits = L0.fbits2;                                                                 \
-      }                                                                                      \
-      if (threadIdx.x == 0) lds[L0.sync + ((t + 1) & 1)] = 0u;  /* the next step's claims */ \
+      if (t & 1) L.stream = L0.stream2;                                                      \
+      c.prev_planes = p.planes ? p.planes - (int64_t)p.B * p.OB : nullptr;                   \
+      c.prev_stream = t > 0 ? lds + ((t & 1) ? L0.stream : L0.stream2) : nullptr;           \
       if (WAB_ROLL_FLOOR) {  /* diagnostic floor: the stores alone (results wrong by design) */ \
         lds_barrier();                                                                       \
         lds_barrier();                                                                       \
       } else {                                                                               \
         __VA_ARGS__;                                                                         \
       }                                                                                      \
-      if (FEAT) step_features<true>(p, L, lds, wave, lane, t);  /* this step's feature bits */ \
+      if (FEAT) step_features<true>(p, L, lds, wave, lane, t);  /* this step's rows */     \
       if (t == T - 1 && p.planes) {                                                          \
         lds_barrier();                                                                       \
         store_units_of<0, 6>(p, lds + L.stream, threadIdx.x);                                \
       }                                                                                      \
-      roll_barrier(roll_pool(p, lds, t), roll_barrier_index(t, 3), lane, true);  /* end: drained */ \
+      lds_barrier();                                                                         \
       ROLL_LOOP_STAMP(38, t == T / 2);  /* past the middle step's end barrier */             \
     }
     if (wave == 0) {
@@ -1598,14 +1529,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
         __builtin_amdgcn_s_setprio(0);
       })
     } else if (wave == 1) {
-      CarryHdr c;
-      WAB_ROLL_STEP(draws_wave<G, true>(p, L, lds, lane, &c, t, t == T - 1))
+      CarryPtr<CarryHdr> c;
+      WAB_ROLL_STEP(draws_wave<G, true>(p, L, lds, lane, &c.c, t, t == T - 1))
     } else if (wave == 2) {
       CarryW2<SLOTS> c;
       WAB_ROLL_STEP((wolves_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1)))
     } else {
-      CarryHdr c;
-      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1)))
+      CarryPtr<CarryHdr> c;
+      WAB_ROLL_STEP((ring_wave<SLOTS, G, true>(p, L, lds, lane, &c.c, t, t == T - 1)))
     }
 #undef WAB_ROLL_STEP
 #undef ROLL_LOOP_STAMP
