@@ -364,7 +364,12 @@ def main():
         desc = desc % seg
         per_launch_steps = seg if c5_roll else 1
         W = max(seg, -(-W // seg) * seg)
-        K = window_steps(K, seg, MIN_TIMED_LAUNCHES if c5_roll else MIN_TIMED_LAUNCHES * seg)
+        if args.policy == "mlp":
+            # closed loop: ~16 graph nodes per step (the policy's kernels and the env launch), so
+            # the captured graph holds 2-4 segments and replays make up the timed window
+            K = min(window_steps(K, seg, 2), 4 * seg)
+        else:
+            K = window_steps(K, seg, MIN_TIMED_LAUNCHES if c5_roll else MIN_TIMED_LAUNCHES * seg)
     elif rollout:
         per_launch_steps = args.rollout
         W = -(-W // args.rollout) * args.rollout
@@ -476,6 +481,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     run(0, W, stream)
     torch.cuda.synchronize(dev)
+    print("bench.py: %d warm-up steps done" % W, file=sys.stderr, flush=True)
     graph = None
     if args.mode == "graph":
         graph = torch.cuda.CUDAGraph()
@@ -486,6 +492,7 @@ def main():
                 run(W, K, torch.cuda.current_stream(dev))
         stream.wait_stream(side)
         torch.cuda.synchronize(dev)
+        print("bench.py: %d steps captured" % K, file=sys.stderr, flush=True)
         # the capture itself did not execute the steps; rewind state by a fresh reset
         env.reset()
         run(0, W, stream)
