@@ -245,8 +245,8 @@ def rollout_wide_report(env, st, g, launches, T):
     names = {"W0": ["start", "despawn/pursuit/grid", "emptied clear + log -> B1", "after B1", "eat/done -> B2",
                     "after B2", "P2 + new episodes"],
              "W1": ["start", "scroll (flag)", "tile value", "after B1", "after B2"],
-             "W2": ["start", "spawn set", "stores -> B1", "stores -> B2", "the rest stored"],
-             "W3": ["start", "strip", "stores -> B1", "stores -> B2", "the rest stored"]}
+             "W2": ["start", "(step 0: tables)", "stores -> B1", "stores -> B2", "the rest stored"],
+             "W3": ["start", "-", "stores -> B1", "stores -> B2", "the rest stored"]}
     acc = {k: [] for k in seqs}
     for it in range(launches):
         st.zero_()
@@ -261,9 +261,12 @@ def rollout_wide_report(env, st, g, launches, T):
             v = s[:, cols]
             ok = (v > 0).all(axis=1)
             acc[k].append((v[ok] - t0[ok, None]).mean(axis=0))
+        acc.setdefault("loop", []).append(((s[:, 0] - s[:, 35]).mean(), (s[:, 38] - t0).mean()))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
+    lp = np.mean(acc["loop"], axis=0) * 10 / 1000
+    print("W0: loop top -> its start %.2f us; step start -> past its end barrier %.2f us" % (lp[0], lp[1]))
 
 
 def rollout_report(env, st, g, launches, T, features=False):

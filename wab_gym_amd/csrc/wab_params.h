@@ -249,7 +249,6 @@ struct WideRollLayout {
   uint32_t bm[2], wp[2], spawn, spw, ring, gap, thr, cval, info, blk, jobEnv, jobKey;
   uint32_t nhdr, act, flag;  // next headers (W0), next actions (W3), hand-off flags
   uint32_t elxy, elrem;      // eaten-log entries 4..kWideRollLog-1 (W0)
-  uint32_t wstrip;           // the entering strip's bits (W3 -> W1)
   uint32_t total;
 };
 
@@ -272,10 +271,9 @@ __host__ __device__ inline WideRollLayout wide_roll_layout(const Params& p) {
   L.jobKey = o; o += 128u;
   L.nhdr = o; o += 64u * 4u;                  // uint4 per env
   L.act = o; o += 16u;                        // 64 int8 actions
-  L.flag = o; o += 4u;  // [0] W1's scroll, [1] W3's strip, [2] W0 at B1 / B2 (step-tagged values)
+  L.flag = o; o += 4u;  // [0] W1's scroll, [1] W2's tables (step 0), [2] W0 at B1 / B2 (step-tagged)
   L.elxy = o; o += 64u * (uint32_t)(kWideRollLog - 4);   // [entry - 4][env] tiles
   L.elrem = o; o += 16u * (uint32_t)(kWideRollLog - 4);  // [entry - 4][env] berries left (bytes)
-  L.wstrip = o; o += 64u;
   L.total = o;
   return L;
 }

@@ -941,6 +941,28 @@ __device__ __forceinline__ void roll_store_row(const Params& p, const uint32_t* 
   while (c.rr >= RPE) { c.rr -= RPE; ++c.e; }
 }
 
+// roll_store_row for the rows whose 128-byte line touches a done env (jm) iff `touching`
+template <uint32_t NT>
+__device__ __forceinline__ void roll_store_row_if(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
+                                                  RowCursor& c, unsigned long long jm, bool touching) {
+  const unsigned long long jn = jm | (jm << 1) | (jm >> 1);  // done envs and their neighbours
+  bool t = false;
+  if ((jn >> c.e) & 1ull) {
+    const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4;
+    const uint32_t n = ((uint32_t)min((int64_t)64, p.B - (int64_t)blockIdx.x * 64)) * CPE;
+    const uint32_t ch = c.e * CPE + c.rr * CPR, c0 = ch & ~7u, c1 = min(c0 + 7u, n - 1u);
+    t = ((jm >> __umulhi(c0, p.magic_CPE)) | (jm >> __umulhi(c1, p.magic_CPE))) & 1ull;  // (chunks < 2^16)
+  }
+  if (t == touching) {
+    roll_store_row<NT>(p, bm, wp, out, c);
+  } else {  // (advance only)
+    const uint32_t RPE = 3u * (uint32_t)p.W;
+    c.q += NT;
+    c.rr += NT;
+    while (c.rr >= RPE) { c.rr -= RPE; ++c.e; }
+  }
+}
+
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
 // (tools/phase_stamps.py --rollout T --config wide31): W0 0..7, W1 8..13, W2 16..20, W3 24..27,
 // the done-env section 36..39
@@ -1001,6 +1023,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   }
 
   for (int t = 0; t < T; ++t) {
+#ifdef WAB_STAMPS
+    if (tid == 0 && p0.stamps && t == T / 2)  // the middle step's loop top
+      p0.stamps[(size_t)blockIdx.x * 40 + 35] = __builtin_amdgcn_s_memrealtime();
+#endif
     const bool last = t == T - 1;
     const int cur = t & 1;
     Params p = kernel_params(p0);
@@ -1023,7 +1049,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     uint4* nhdr = reinterpret_cast<uint4*>(lds + L.nhdr);
     uint32_t* act = lds + L.act;
     uint32_t* flag = lds + L.flag;
-    uint32_t* wstrip = lds + L.wstrip;
     uint32_t* elxy = lds + L.elxy;
     uint8_t* elrem = reinterpret_cast<uint8_t*>(lds + L.elrem);
     const uint32_t OB = (uint32_t)p.OB;
@@ -1162,6 +1187,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         }
       }
       kill = kill && !p.god_mode;
+      // spawn_wolves (:527-576): the ring's spawn set this turn (one draw unless a wolf spawns),
+      // read by this lane only (P2); step 0: once W2 has the gap table in LDS
+      for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
+      if (p.wolves_on) {
+        if (t == 0) lds_await_step(p, flag + 1, 1u);
+        if (active)
+          spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0,
+                     h.b1, [&](int r) { spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31); });
+      }
       ROLLW_STAMP(1);
       // emptied tiles that scrolled back into view are absent from S (:506): cleared from the
       // bitmap once W1 has scrolled it (the per-step kernel's W1 does this from its own loads)
@@ -1391,8 +1425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         eaten_empty = active && !((jmp >> lane) & 1ull) && (info[lane] & 2u);
       }
       const uint32_t ccw = eaten_empty ? ~(1u << p.ch) : ~0u;
-      lds_await_step(p, flag + 1, (uint32_t)t + 1u);  // the strip, drawn by W3 meanwhile
-      const uint32_t strip = wstrip[lane];
+      const uint32_t strip = active ? strip_bits(p, h) : 0u;  // generate_bushes (:613-629)
       const uint32_t hmask = p.H >= 32 ? ~0u : ((1u << p.H) - 1u);
       const uint32_t top = 1u << (p.H - 1);
       const int Wv = p.W, cwv = p.cw;
@@ -1440,26 +1473,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       lds_barrier();  // B2
       ROLLW_STAMP(12);
     } else {
-      // ---------------------------------------------- W3: the strip for W1; W2: tables, spawn set;
-      // then both store the last step's obs
-      if (wave == 3) {  // the entering strip's draws, for W1's scroll
-        wstrip[lane] = active ? strip_bits(p, h) : 0u;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // ---------------------------------------------- W2, W3: the store waves (step 0: W2 loads
+      // the spawn tables for W0 first)
+      if (wave == 2 && t == 0) {
+        copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
+        if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
+        __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) lds_publish_step(flag + 1, (uint32_t)t + 1u);
-      } else {
-        if (t == 0) {
-          copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
-          if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
-          __builtin_amdgcn_s_waitcnt(0);
-        }
-        for (int w = 0; w < RW; ++w) spawn[(uint32_t)lane * L.spw + (uint32_t)w] = 0u;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (p.wolves_on && active)
-          spawn_hits(gap, p.R, p.gap_full_th, p.gap_full_tl, p.gap_ring_th, p.gap_ring_tl, p.gap_inv_l2, h.turn, h.b0, h.b1, [&](int r) {
-            spawn[(uint32_t)lane * L.spw + ((uint32_t)r >> 5)] |= 1u << (r & 31);
-          });
+        if (lane == 0) lds_publish_step(flag + 1, 1u);  // (W0 waits for the tables once)
       }
       ROLLW_STAMP(8 * wave + 1);
       RowCursor rc = row_cursor(p, (uint32_t)(tid - 128));  // (thread tid - 128 of the two store waves)
@@ -1480,6 +1501,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       lds_barrier();  // B2
       if (t > 0)  // ... and the rest, while W0 and W1 build the new episodes
         while (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+      if (last) {  // this step's S lines that touch no done env are final: out now (the rest after
+                   // the new episodes, below)
+        const unsigned long long jm = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+        RowCursor c = row_cursor(p, (uint32_t)(tid - 128));
+        while (c.q < n_rows) roll_store_row_if<128>(p, bm, wp, out, c, jm, false);
+      }
       ROLLW_STAMP(8 * wave + 4);
     }
 
@@ -1571,11 +1598,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     if (wave == 0) ROLLW_STAMP(39);
     if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
     lds_barrier();  // the step's end: its obs buffers are complete; the next step's inputs are in
+#ifdef WAB_STAMPS
+    if (tid == 0 && p0.stamps && t == T / 2)  // past the middle step's end barrier
+      p0.stamps[(size_t)blockIdx.x * 40 + 38] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (last) {
-      // the last step's obs, by all 256 threads; every env's bitmap rows (continuing: post-eat;
-      // done: the new episode's)
-      RowCursor c = row_cursor(p, (uint32_t)tid);
-      while (c.q < n_rows) roll_store_row<256>(p, bm, wp, out, c);
+      // the last step's obs lines that touch a done env (its new episode, its neighbours' S), by
+      // all 256 threads; every env's bitmap rows (continuing: post-eat; done: the new episode's)
+      if (jmask) {
+        RowCursor c = row_cursor(p, (uint32_t)tid);
+        while (c.q < n_rows) roll_store_row_if<256>(p, bm, wp, out, c, jmask, true);
+      }
       for (uint32_t u = tid; u < 64u * 32u; u += 256) {
         const uint32_t e = u >> 5, i = u & 31u;
         if ((int)e >= n_active || i >= (uint32_t)p.W) continue;
