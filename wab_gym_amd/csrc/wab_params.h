@@ -271,7 +271,8 @@ __host__ __device__ inline WideRollLayout wide_roll_layout(const Params& p) {
   L.jobKey = o; o += 128u;
   L.nhdr = o; o += 64u * 4u;                  // uint4 per env
   L.act = o; o += 16u;                        // 64 int8 actions
-  L.flag = o; o += 4u;  // [0] W1's scroll, [1] W2's tables (step 0), [2] W0 at B1 / B2 (step-tagged)
+  L.flag = o; o += 8u;  // [0] W1's scroll, [1] W2's tables (step 0), [2] W0 at B1 / B2 (step-tagged),
+                        // [4], [5] the obs-row queues' block counters (by step parity)
   L.elxy = o; o += 64u * (uint32_t)(kWideRollLog - 4);   // [entry - 4][env] tiles
   L.elrem = o; o += 16u * (uint32_t)(kWideRollLog - 4);  // [entry - 4][env] berries left (bytes)
   L.total = o;

@@ -849,9 +849,6 @@ __device__ __forceinline__ void lds_await_step(const Params& p, const uint32_t* 
   }
   atomicAdd(&p.counters[CTR_HANDOFF_TIMEOUTS], 1ull);
 }
-__device__ __forceinline__ bool lds_reached(const uint32_t* flag, uint32_t v) {  // (wave-uniform)
-  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= v;
-}
 
 // whead of a carried header and action
 __device__ __forceinline__ WHead whead_of(const Params& p, int64_t g, bool active, uint4 hdr, int a) {
@@ -941,6 +938,53 @@ __device__ __forceinline__ void roll_store_row(const Params& p, const uint32_t* 
   while (c.rr >= RPE) { c.rr -= RPE; ++c.e; }
 }
 
+// Obs rows by blocks of 64 (one wave-instruction pair per block, 16 whole 128-byte lines),
+// claimed from a per-step LDS counter by whichever wave has nothing else to do, so that the
+// store stream is spread over every idle wave and no wave ends its share much later than the
+// others.  A queue: the rows of one step, [0, n_rows), its counter, and the done envs' mask when
+// only the lines that touch no done env are wanted (the last step's S after B2).
+struct RowQueue {
+  uint32_t* ctr;
+  uint32_t n_rows, n_blocks, magic;  // magic: row -> env division (umulhi, exact below 2^16 rows)
+  const uint32_t* bm;
+  const uint32_t* wp;
+  uint8_t* out;
+  unsigned long long jm;
+  bool untouched_only;
+};
+__device__ __forceinline__ RowQueue row_queue(const Params& p, uint32_t* ctr, uint32_t n_rows, const uint32_t* bm,
+                                              const uint32_t* wp, uint8_t* out) {
+  RowQueue q;
+  q.ctr = ctr;
+  q.n_rows = n_rows;
+  q.n_blocks = (n_rows + 63u) >> 6;
+  const uint32_t RPE = 3u * (uint32_t)p.W;
+  q.magic = (uint32_t)((0x100000000ull + RPE - 1u) / RPE);
+  q.bm = bm;
+  q.wp = wp;
+  q.out = out;
+  q.jm = 0ull;
+  q.untouched_only = false;
+  return q;
+}
+template <bool IF>
+__device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, uint32_t b, int lane);
+
+// claim and store blocks until the queue is empty (true) or flag >= v (v > 0; false)
+__device__ __forceinline__ bool drain_rows(const Params& p, const RowQueue& q, int lane, const uint32_t* flag = nullptr,
+                                           uint32_t v = 0u) {
+  while (true) {
+    if (v && __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= v)
+      return false;
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(q.ctr, 1u);
+    b = (uint32_t)__shfl((int)b, 0);
+    if (b >= q.n_blocks) return true;
+    if (q.untouched_only) store_block<true>(p, q, b, lane);
+    else store_block<false>(p, q, b, lane);
+  }
+}
+
 // roll_store_row for the rows whose 128-byte line touches a done env (jm) iff `touching`
 template <uint32_t NT>
 __device__ __forceinline__ void roll_store_row_if(const Params& p, const uint32_t* bm, const uint32_t* wp, uint8_t* out,
@@ -961,6 +1005,27 @@ __device__ __forceinline__ void roll_store_row_if(const Params& p, const uint32_
     c.rr += NT;
     while (c.rr >= RPE) { c.rr -= RPE; ++c.e; }
   }
+}
+
+// the last step's queue after B2: its S lines that touch no done env (blk: the job mask)
+__device__ __forceinline__ RowQueue untouched_rows(const Params& p, uint32_t* ctr, uint32_t n_rows, const uint32_t* bm,
+                                                   const uint32_t* wp, uint8_t* out, const uint32_t* blk) {
+  RowQueue q = row_queue(p, ctr, n_rows, bm, wp, out);
+  q.jm = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
+  q.untouched_only = true;
+  return q;
+}
+
+template <bool IF>
+__device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, uint32_t b, int lane) {
+  const uint32_t row = 64u * b + (uint32_t)lane;
+  if (row >= q.n_rows) return;
+  RowCursor c;
+  c.q = row;
+  c.e = __umulhi(row, q.magic);
+  c.rr = row - c.e * 3u * (uint32_t)p.W;
+  if (IF) roll_store_row_if<64>(p, q.bm, q.wp, q.out, c, q.jm, false);
+  else roll_store_row<64>(p, q.bm, q.wp, q.out, c);
 }
 
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
@@ -1018,7 +1083,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   uint32_t lxy[4] = {0u, 0u, 0u, 0u}, lrem[4] = {0u, 0u, 0u, 0u};
   {  // the step flags start below every step's value
     const WideRollLayout L = wide_roll_layout(p0);
-    if (tid < 4) lds[L.flag + tid] = 0u;
+    if (tid < 8) lds[L.flag + tid] = 0u;
     lds_barrier();
   }
 
@@ -1058,26 +1123,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     // the W0 -> store-wave phase signals of this step (flag[2]): B1 reached, B2 reached
     const uint32_t at_b1 = 2u * (uint32_t)t + 1u, at_b2 = 2u * (uint32_t)t + 2u;
     const uint32_t n_rows = (uint32_t)n_active * 3u * (uint32_t)p.W;  // the group's obs rows per step
+    // step t - 1's rows, stored during this step (row-block counter flag[4 + (t - 1) % 2]); this
+    // step's counter is cleared now (last used two steps ago)
+    const RowQueue qp = row_queue(p, flag + 4 + ((t + 1) & 1), n_rows, bm_prev, wp_prev, out_prev);
+    if (tid == 0) flag[4 + cur] = 0u;
 
-    int a = 0;
-    if (t == 0) {
-      if (active) {
-        hdr = p.hdr[g];
-        a = (int)p.actions[g];
+    WHead h = {};  // (the header and action: W0 and W1 only)
+    if (wave < 2) {
+      int a = 0;
+      if (t == 0) {
+        if (active) {
+          hdr = p.hdr[g];
+          a = (int)p.actions[g];
+        }
+        // (every step-0 load settled inside its branch: the waitcnt pass would otherwise put
+        // vmcnt(0) waits at the join that every later step executes too, each one waiting for all
+        // of the wave's obs stores in flight)
+        __builtin_amdgcn_s_waitcnt(0);
+      } else {
+        hdr = nhdr[lane];
+        a = (int)reinterpret_cast<const int8_t*>(act)[lane];
       }
-      // (every step-0 load settled inside its branch: the waitcnt pass would otherwise put
-      // vmcnt(0) waits at the join that every later step executes too, each one waiting for all
-      // of the wave's obs stores in flight)
-      __builtin_amdgcn_s_waitcnt(0);
-    } else {
-      hdr = nhdr[lane];
-      a = (int)reinterpret_cast<const int8_t*>(act)[lane];
+      h = whead_of(p, g, active, hdr, a);
     }
-    const WHead h = whead_of(p, g, active, hdr, a);
-    if (WAB_WIDE_ROLL_FLOOR) {  // (diagnostic floor: the store waves' stores alone; results wrong)
-      RowCursor rc = row_cursor(p, (uint32_t)(tid - 128));
-      if (wave >= 2 && t > 0)
-        while (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
+    if (WAB_WIDE_ROLL_FLOOR) {  // (diagnostic floor: the stores alone, every wave; results wrong)
+      if (t > 0) drain_rows(p, qp, lane);
       lds_barrier();
       continue;
     }
@@ -1470,6 +1540,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       ROLLW_STAMP(10);
       lds_barrier();  // B1
       ROLLW_STAMP(11);
+      if (t > 0) drain_rows(p, qp, lane, flag + 2, at_b2);  // (idle until B2: store)
       lds_barrier();  // B2
       ROLLW_STAMP(12);
     } else {
@@ -1483,30 +1554,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         if (lane == 0) lds_publish_step(flag + 1, 1u);  // (W0 waits for the tables once)
       }
       ROLLW_STAMP(8 * wave + 1);
-      RowCursor rc = row_cursor(p, (uint32_t)(tid - 128));  // (thread tid - 128 of the two store waves)
-      if (t > 0)  // step t - 1's rows until W0 reaches B1 (two rows per check)
-        while (rc.q < n_rows && !lds_reached(flag + 2, at_b1)) {
-          roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
-          if (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
-        }
+      if (t > 0) drain_rows(p, qp, lane, flag + 2, at_b1);  // step t - 1's rows until W0 reaches B1
       ROLLW_STAMP(8 * wave + 2);
       lds_barrier();  // B1
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
-      if (t > 0)  // ... until W0 reaches B2
-        while (rc.q < n_rows && !lds_reached(flag + 2, at_b2)) {
-          roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
-          if (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
-        }
+      if (t > 0) drain_rows(p, qp, lane, flag + 2, at_b2);  // ... until W0 reaches B2
       ROLLW_STAMP(8 * wave + 3);
       lds_barrier();  // B2
-      if (t > 0)  // ... and the rest, while W0 and W1 build the new episodes
-        while (rc.q < n_rows) roll_store_row<128>(p, bm_prev, wp_prev, out_prev, rc);
-      if (last) {  // this step's S lines that touch no done env are final: out now (the rest after
-                   // the new episodes, below)
-        const unsigned long long jm = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
-        RowCursor c = row_cursor(p, (uint32_t)(tid - 128));
-        while (c.q < n_rows) roll_store_row_if<128>(p, bm, wp, out, c, jm, false);
-      }
+      if (t > 0) drain_rows(p, qp, lane);  // ... the rest, while W0 and W1 build the new episodes
+      if (last) drain_rows(p, untouched_rows(p, flag + 4 + cur, n_rows, bm, wp, out, blk), lane);
       ROLLW_STAMP(8 * wave + 4);
     }
 
@@ -1594,6 +1650,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           p.food[g] = food2;
         }
       }
+    }
+    if (wave < 2) {  // W0 and W1 are done with the step: they store too
+      if (t > 0) drain_rows(p, qp, lane);
+      if (last) drain_rows(p, untouched_rows(p, flag + 4 + cur, n_rows, bm, wp, out, blk), lane);
     }
     if (wave == 0) ROLLW_STAMP(39);
     if (wave == 0 && wolf_of) atomicAdd(&p.counters[CTR_WOLF_OVERFLOW], wolf_of);
