@@ -938,7 +938,6 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   const uint32_t info = s.info[lane];
   const bool killed = s.kill[lane] != 0u;
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(info), killed);
-  if (ROLL && !last) prefetch_actions(p, s, lane);  // the next step's (in LDS by the step's end)
   // the reset draws of the done envs for view cells [0, 64); W3 draws the rest and waits for
   // flag[1] before it builds the new episodes
   const unsigned long long jm = __ballot(job);
@@ -960,6 +959,9 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     // needed only at B2, so after the reset draws W3 waits for
     render_s(p, s, lane, info, h.dir);
   }
+  // the next step's actions (in LDS by the step's end), after the draws W3 waits for: the
+  // scalar load's wait is then off that chain
+  if (ROLL && !last) prefetch_actions(p, s, lane);
   SMALL_STAMP(13);
   lds_barrier();  // B2
   if (p.t_planes) lds_barrier();  // B3

@@ -957,7 +957,7 @@ __device__ __forceinline__ RowQueue row_queue(const Params& p, uint32_t* ctr, ui
   RowQueue q;
   q.ctr = ctr;
   q.n_rows = n_rows;
-  q.n_blocks = (n_rows + 63u) >> 6;
+  q.n_blocks = (n_rows * ((uint32_t)p.S >> 4) + 63u) >> 6;  // blocks of 64 16-byte chunks
   const uint32_t RPE = 3u * (uint32_t)p.W;
   q.magic = (uint32_t)((0x100000000ull + RPE - 1u) / RPE);
   q.bm = bm;
@@ -1016,16 +1016,29 @@ __device__ __forceinline__ RowQueue untouched_rows(const Params& p, uint32_t* ct
   return q;
 }
 
+// Block b of a queue: lane l stores 16-byte chunk 64 b + l of the group's obs (one row half when
+// rows are 32 bytes), non-temporal, so each wave-instruction writes 1 KiB contiguous, eight
+// whole lines.  (Measured at B = 65536, T = 64, one box: rows per lane, the two halves from
+// two back-to-back instructions, 40.4-40.7 us per step, non-temporal 102 us (partial lines);
+// chunks 39.7, non-temporal chunks 38.9; the pattern's stores alone 34.1-35.9.)
 template <bool IF>
 __device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, uint32_t b, int lane) {
-  const uint32_t row = 64u * b + (uint32_t)lane;
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W;
+  const uint32_t ch = 64u * b + (uint32_t)lane, row = CPR == 2u ? ch >> 1 : ch, half = CPR == 2u ? ch & 1u : 0u;
   if (row >= q.n_rows) return;
-  RowCursor c;
-  c.q = row;
-  c.e = __umulhi(row, q.magic);
-  c.rr = row - c.e * 3u * (uint32_t)p.W;
-  if (IF) roll_store_row_if<64>(p, q.bm, q.wp, q.out, c, q.jm, false);
-  else roll_store_row<64>(p, q.bm, q.wp, q.out, c);
+  const uint32_t e = __umulhi(row, q.magic), rr = row - e * 3u * W;
+  if (IF) {  // (only the lines that touch no done env)
+    const unsigned long long jn = q.jm | (q.jm << 1) | (q.jm >> 1);
+    if ((jn >> e) & 1ull) {
+      const uint32_t n = ((uint32_t)min((int64_t)64, p.B - (int64_t)blockIdx.x * 64)) * CPE;
+      const uint32_t c0 = (e * CPE + rr * CPR) & ~7u, c1 = min(c0 + 7u, n - 1u);
+      if (((q.jm >> __umulhi(c0, p.magic_CPE)) | (q.jm >> __umulhi(c1, p.magic_CPE))) & 1ull) return;
+    }
+  }
+  const uint32_t k = (rr >= W ? 1u : 0u) + (rr >= 2u * W ? 1u : 0u);
+  const uint32_t i = rr - k * W;
+  const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? 1u << p.ch : 0u) : (k == 0u ? q.wp : q.bm)[e * kRollPitch + i];
+  __builtin_nontemporal_store(expand16((v >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(q.out) + e * CPE + rr * CPR + half);
 }
 
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
@@ -1146,8 +1159,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       }
       h = whead_of(p, g, active, hdr, a);
     }
-    if (WAB_WIDE_ROLL_FLOOR) {  // (diagnostic floor: the stores alone, every wave; results wrong)
-      if (t > 0) drain_rows(p, qp, lane);
+    if (WAB_WIDE_ROLL_FLOOR) {  // (diagnostic floor: the stores alone, every wave (2: W2, W3); results wrong)
+      if (t > 0 && (WAB_WIDE_ROLL_FLOOR == 1 || wave >= 2)) drain_rows(p, qp, lane);
       lds_barrier();
       continue;
     }
