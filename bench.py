@@ -298,6 +298,9 @@ def main():
                          "[B] buffer rewritten every step (which a 256 MB Infinity Cache can absorb)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-diag", action="store_true",
+                    help="skip the diagnostic launches beside the line (per-step launches, single-launch "
+                         "timings): for profiling the line's kernel alone")
     ap.add_argument("--wolf-slots", type=int, default=0, choices=[0, 8, 16, 32],
                     help="override the config's wolf rows per env (0: the config's own; the wide "
                          "kernel keeps 8 of them in registers)")
@@ -548,7 +551,7 @@ def main():
     # figure rocprofv3's average agrees with); events bracketing single launches (below, not
     # timed above) add their own overhead and are reported as a diagnostic only
     kern_ms = stream_ms / K
-    n_k = min(K_req, 200)  # (the actions buffer holds W + K_req steps)
+    n_k = min(K_req, 200) if not args.no_diag else 0  # (the actions buffer holds W + K_req steps)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_k)]
     s = ctypes.c_void_p(stream.cuda_stream)
     for i in range(n_k):
@@ -556,7 +559,7 @@ def main():
         L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s)
         evs[i][1].record(stream)
     torch.cuda.synchronize(dev)
-    single_ms = sorted(a.elapsed_time(b) for a, b in evs)[n_k // 2]
+    single_ms = sorted(a.elapsed_time(b) for a, b in evs)[n_k // 2] if n_k else float("nan")
     kernel_name = "wab_step_%s (fused step)" % L.wab_step_kernel(h).decode()
     alg = alg_bytes_per_env_step(env.W, env.H)
     c5_line = None
@@ -565,7 +568,10 @@ def main():
     # a kernel's average launch from n back-to-back launches of it alone, captured in a graph
     # (as the timed region is) so that host launch cost does not pace a short kernel; HIP
     # events on the launch stream around one replay
-    def per_launch(fn, n):
+    def per_launch(fn, n, required=False):
+        if args.no_diag and not required:
+            return float("nan")
+
         def launches(st):
             sc = ctypes.c_void_p(st.cuda_stream)
             for i in range(n):
@@ -625,7 +631,8 @@ def main():
         ret_ms = per_launch(lambda i, s: L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s), 64)
         if fused:
             sf_ms = per_launch(lambda i, s: L.wab_step_features(h, a0 + (W + i) * B, fobs_addr, rew, done,
-                                                                f0 + 4 * (i % T) * B * F, s), n_k)
+                                                                f0 + 4 * (i % T) * B * F, s), n_k,
+                               required=not c5_roll)
             # per env-step: the step's bytes without the planes (never stored), the F floats
             sf_alg = alg - 3 * env.W * env.H + 4 * F
             c5_line = {"segment": T, "feature_dim": F, "fused": True,

@@ -1,0 +1,23 @@
+"""profiles/traffic_<config>_rollout<T>_b<B>.json (bench.py's roofline.traffic and .valu) from a
+tools/summarize_profile.py summary:
+    python tools/traffic_json.py profiles/<tag>/summary.json <config> <T> <B> <alg bytes per env-step>"""
+import json
+import sys
+
+
+def main(summary, config, T, B, alg_per_env_step):
+    s = json.load(open(summary))
+    T, B, alg = int(T), int(B), float(alg_per_env_step)
+    hbm = s["hbm_bytes_per_launch"]
+    alg_launch = alg * B * T
+    out = {"config": "%s rollout (T=%d), B=%d" % (config, T, B), "kernel": s["trace"]["name"],
+           "avg_ns": s["trace"]["avg_ns"], "hbm_bytes_per_launch": hbm, "alg_bytes_per_launch": alg_launch,
+           "traffic_over_alg": hbm["total_corrected"] / alg_launch, "valu": s.get("valu"),
+           "source": summary.rsplit("/", 1)[0]}
+    path = "profiles/traffic_%s_rollout%d_b%d.json" % (config, T, B)
+    json.dump(out, open(path, "w"), indent=1)
+    print(path, json.dumps({k: out[k] for k in ("avg_ns", "traffic_over_alg")}))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
