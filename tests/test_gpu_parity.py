@@ -1036,3 +1036,38 @@ def test_rollout_features_ambiguous_rewards_fail_before_stepping():
     assert r["returns"] is not None
     r = env.rollout_features(a, returns=False)
     assert r["returns"] is None and env.counters()["steps"] == steps0 + 194 * 256
+
+
+def test_wide_step_into_alternating_buffers():
+    """The wide view's wab_step picks its kernel by the obs buffer (the last step's: the per-step
+    kernel; another: the rollout build with one step): steps alternating between two obs
+    buffers (and back to one) switch kernels every step and still match the oracle bit for bit."""
+    import ctypes
+
+    import torch
+
+    from wab_gym_amd import _lib
+
+    opts = {"width": 31, "height": 31}
+    n = 1024
+    env = _env(opts, n, plane_stride=32, wolf_slots=32, validate_actions=False)
+    orc = _oracle(opts, n, stride=32)
+    env.reset()
+    orc.reset()
+    assert env.step_kernel == "wide"
+    bufs = [env._alloc_obs() for _ in range(2)]
+    L = _lib.load()
+    rng = np.random.RandomState(21)
+    for t in range(120):
+        a = rng.randint(5, size=n)
+        o = bufs[t % 2] if t < 80 else bufs[0]
+        ad = torch.as_tensor(a.astype(np.int8), device="cuda:0")
+        _lib.check(L.wab_step(env._h, ad.data_ptr(), ctypes.addressof(o["struct"]), env.reward.data_ptr(),
+                              env.done.data_ptr(), None, env._stream()), "wab_step")
+        op, of, orl, ost, orew, odone = orc.step(a, nthreads=16)
+        assert np.array_equal(o["planes"].cpu().numpy(), op), t
+        assert np.array_equal(o["scalars"].cpu().numpy(), np.stack([of, orl, ost])), t
+        assert np.array_equal(env.reward.cpu().numpy(), orew), t
+        assert np.array_equal(env.done.cpu().numpy(), odone), t
+    c = env.counters()
+    assert c["wolf_overflow"] == 0 and c["handoff_timeouts"] == 0 and c["steps"] == 120 * n
