@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
   struct Cfg { unsigned blocks, threads; bool nt; };
   std::vector<Cfg> cfgs = {{1024, 256, true}, {1024, 256, false}, {1024, 192, true}, {2048, 256, true},
                            {4096, 256, true}, {8192, 256, true}, {512, 256, true}, {256, 256, true},
-                           {16384, 256, true}};
+                           {16384, 256, true}, {4096, 256, false}, {8192, 256, false}, {16384, 256, false}};
   for (const Cfg& c : cfgs) {
     const unsigned per_block = (unsigned)(total / 16 / c.blocks);
     float best = 1e9f;

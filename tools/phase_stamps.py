@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--build-only", action="store_true", help="build the stamps library and exit (CPU side)")
     ap.add_argument("--no-build", action="store_true", help="use the prebuilt stamps library (GPU box)")
     ap.add_argument("--lib", default=OUT, help="the stamps library to load (with --no-build)")
+    ap.add_argument("--out", default=OUT, help="where --build-only writes the library")
+    ap.add_argument("--cflags", default="", help="extra hipcc flags of the stamps build (A/B variants)")
     ap.add_argument("--b2b", type=int, default=0,
                     help="instead: per-XCD entry/end of the last two of N back-to-back launches")
     ap.add_argument("--rollout", type=int, default=0,
@@ -37,7 +39,8 @@ def main():
 
     if not args.no_build:
         src = [os.path.join(ge.CSRC, s) for s in ge.HIP_SOURCES]
-        subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS", "-o", OUT] + src, check=True)
+        subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS"] + args.cflags.split()
+                       + ["-o", args.out] + src, check=True)
     if args.build_only:
         return
     os.environ["WAB_LIB"] = args.lib if args.no_build else OUT
@@ -262,11 +265,22 @@ def rollout_wide_report(env, st, g, launches, T):
             ok = (v > 0).all(axis=1)
             acc[k].append((v[ok] - t0[ok, None]).mean(axis=0))
         acc.setdefault("loop", []).append(((s[:, 0] - s[:, 35]).mean(), (s[:, 38] - t0).mean()))
+        ent, ex = s[:, 32], s[:, 34]
+        xcc = s[:, 33]
+        acc.setdefault("xcd", []).append([(ex - ent)[xcc == x].mean() if (xcc == x).any() else 0.0 for x in range(8)])
+        acc.setdefault("quart", []).append([q.mean() for q in np.array_split(ex - ent, 8)])
+        acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean(), np.percentile(ent - ent.min(), 99),
+                                             np.percentile(ex - ent.min(), 1), np.percentile(ex - ent.min(), 50)))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
     lp = np.mean(acc["loop"], axis=0) * 10 / 1000
     print("W0: loop top -> its start %.2f us; step start -> past its end barrier %.2f us" % (lp[0], lp[1]))
+    la = np.mean(acc["launch"], axis=0) * 10 / 1000
+    print("workgroup entry -> exit by XCD (us):", np.round(np.mean(acc["xcd"], axis=0) * 10 / 1000, 1))
+    print("workgroup entry -> exit by blockIdx eighth (us):", np.round(np.mean(acc["quart"], axis=0) * 10 / 1000, 1))
+    print("launch: first entry -> last exit %.1f us (%.2f us per step); workgroup entry -> exit mean %.1f us; "
+          "entries p99 %.1f us after the first; exits p1 %.1f, p50 %.1f us" % (la[0], la[0] / T, la[1], la[2], la[3], la[4]))
 
 
 def rollout_report(env, st, g, launches, T, features=False):
@@ -307,6 +321,10 @@ def rollout_report(env, st, g, launches, T, features=False):
             acc[k].append((v[ok] - t0[ok, None]).mean(axis=0))
         spans.append((s[:, [5, 14, 20, 26]].max(axis=1) - t0).mean())
         acc.setdefault("loop", []).append(((s[:, 0] - s[:, 35]).mean(), (s[:, 38] - t0).mean()))
+        ent, ex, xcc = s[:, 32], s[:, 39], s[:, 33]
+        acc.setdefault("xcd", []).append([(ex - ent)[xcc == x].mean() if (xcc == x).any() else 0.0 for x in range(8)])
+        acc.setdefault("eighth", []).append([q.mean() for q in np.array_split(ex - ent, 8)])
+        acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean()))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
@@ -314,6 +332,11 @@ def rollout_report(env, st, g, launches, T, features=False):
     lp = np.mean(acc["loop"], axis=0) * 10 / 1000
     print("W0: loop top -> its start (parameters, slices) %.2f us; step start -> past its end barrier %.2f us"
           % (lp[0], lp[1]))
+    la = np.mean(acc["launch"], axis=0) * 10 / 1000
+    print("launch: first entry -> last exit %.1f us (%.2f us per step); workgroup entry -> exit mean %.1f us"
+          % (la[0], la[0] / T, la[1]))
+    print("workgroup entry -> exit by XCD (us):", np.round(np.mean(acc["xcd"], axis=0) * 10 / 1000, 1))
+    print("workgroup entry -> exit by blockIdx eighth (us):", np.round(np.mean(acc["eighth"], axis=0) * 10 / 1000, 1))
     if features:
         f = np.mean(acc["feat"], axis=0) * 10 / 1000
         print("features: emitted %.2f, wave 0's row stores issued %.2f us" % (f[0], f[1]))

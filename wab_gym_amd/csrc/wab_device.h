@@ -301,6 +301,14 @@ __device__ __forceinline__ void lds_await(const Params& p, const uint32_t* flag)
 // Workgroup barrier for LDS hand-offs only.  Waves of a block exchange data exclusively
 // through LDS; __syncthreads() would also drain every outstanding global store
 // (s_waitcnt vmcnt(0)) and put HBM write latency on the critical path of each phase.
+// s_setprio takes an immediate: a wave-uniform run-time level through a branch
+__device__ __forceinline__ void set_prio_dyn(uint32_t pr) {
+  if (pr == 0u) __builtin_amdgcn_s_setprio(0);
+  else if (pr == 1u) __builtin_amdgcn_s_setprio(1);
+  else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
+  else __builtin_amdgcn_s_setprio(3);
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

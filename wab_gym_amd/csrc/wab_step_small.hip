@@ -1542,6 +1542,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     }
 #undef WAB_ROLL_STEP
 #undef ROLL_LOOP_STAMP
+#ifdef WAB_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && p0.stamps)  // every store of the workgroup retired (slot 39)
+      p0.stamps[(size_t)blockIdx.x * 40 + 39] = __builtin_amdgcn_s_memrealtime();
+#endif
   }
 }
 

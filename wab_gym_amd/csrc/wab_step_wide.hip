@@ -1072,6 +1072,7 @@ __device__ __forceinline__ void wide_step_slice(Params& p, int t) {
 
 }  // namespace
 
+
 template <int SLOTS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wab_rollout_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1079,6 +1080,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   if (g0 >= p0.B) return;  // (uniform over the workgroup)
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int T = p0.n_steps;
+#ifdef WAB_STAMPS
+  if (tid == 0 && p0.stamps) {  // kernel entry (slot 32), the XCD (33)
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    p0.stamps[(size_t)blockIdx.x * 40 + 32] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
+  }
+#endif
   const int n_active = (int)min((int64_t)64, p0.B - g0);
   const int64_t g = g0 + lane;
   const bool active = lane < n_active;
@@ -1559,6 +1568,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     } else {
       // ---------------------------------------------- W2, W3: the store waves (step 0: W2 loads
       // the spawn tables for W0 first)
+      // Issue priority rotating over the four co-resident workgroups of a CU (blockIdx b,
+      // b + 256, b + 512, b + 768, dispatched in that order): at equal priority the arbiter
+      // favours the oldest wave, so the youngest group's stores fell behind and its CU ran the
+      // launch's tail alone (group durations by dispatch quarter 1720, 1930, 2170, 2440 us;
+      // rotating: 1965, 2070, 2174, 2304).  C3 T = 64: 2728-2737 -> 2618-2628 us per launch
+      // (tools/ab_wide.sh; every wave rotating: 2609-2633; static inverse-age priority 2786).
+      set_prio_dyn(((blockIdx.x >> 8) + (uint32_t)t) & 3u);
       if (wave == 2 && t == 0) {
         copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
         if (p.wolves_on) copy_to_lds(gap, p.gap, p.n_gap + 1, lane);
@@ -1691,6 +1707,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       }
     }
   }
+#ifdef WAB_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0 && p0.stamps)  // every store of the workgroup retired (slot 34)
+    p0.stamps[(size_t)blockIdx.x * 40 + 34] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 template __global__ void wab_rollout_wide<8>(Params);
