@@ -28,6 +28,7 @@
  *                               + finish_episode's returns              actor_critic.py:139-143
  *   wab_render            <- WolvesAndBushesEnv.render (rgb_array,   wab_env.py:468-502
  *                            draw_health text included)
+ *   wab_render_envs       <- the same for a range of envs (Monitor video frames)
  *   wab_egocentric        <- WolvesAndBushesEnvEgoCentric._get_obs /  wab_env.py:930-979
  *                            _get_bush_proximities                   wab_env.py:652-667
  *                            + gym.spaces.flatten                    actor_critic.py:188
@@ -259,6 +260,11 @@ int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features,
  * is drawn at (0, 0) in blue with the digit glyphs of PIL's default font (wab_glyphs.h). */
 int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, int32_t draw_health, uint8_t* rgb,
                void* stream);
+/* The same for envs [first, first + count) of the observation only: rgb [count][W*scale]
+ * [H*scale][3] (one env's frames for the Monitor's video recorder, gym.wrappers.Monitor
+ * via wab_env.py:1013, actor_critic.py:46). */
+int wab_render_envs(wab_handle* h, const wab_obs* obs, int64_t first, int64_t count, int32_t scale,
+                    int32_t draw_health, uint8_t* rgb, void* stream);
 
 /* Bush proximities of the egocentric env variants (WolvesAndBushesEnvEgoCentric and
  * WolvesAndBushesEnvEgocentricJustBushes, wab_env.py:930-979) for the handle's current state:

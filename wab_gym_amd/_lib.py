@@ -18,7 +18,7 @@ EXPORTED = [
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
     "wab_debug_bush_values", "wab_step_features", "wab_discounted_returns_exact",
-    "wab_bush_thresholds", "wab_rollout_features",
+    "wab_bush_thresholds", "wab_rollout_features", "wab_render_envs",
 ]
 
 ABI_VERSION = 4
@@ -73,6 +73,7 @@ def load():
     L.wab_featurize_superbasic.argtypes = [P, P, P, P]
     L.wab_step_features.argtypes = [P, P, P, P, P, P, P]
     L.wab_render.argtypes = [P, P, I32, I32, P, P]
+    L.wab_render_envs.argtypes = [P, P, I64, I64, I32, I32, P, P]
     L.wab_egocentric.argtypes = [P, P, P, P]
     L.wab_debug_bush_values.argtypes = [P, P, P, I64, P]
     L.wab_discounted_returns.argtypes = [P, P, I32, I64, ctypes.c_double, P, P, P]

@@ -992,9 +992,18 @@ int wab_featurize_superbasic(wab_handle* h, const wab_obs* obs, float* features,
 
 int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, int32_t draw_health, uint8_t* rgb, void* stream) {
   g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_render: NULL argument");
+  return wab_render_envs(h, obs, 0, h->p.B, scale, draw_health, rgb, stream);
+}
+
+int wab_render_envs(wab_handle* h, const wab_obs* obs, int64_t first, int64_t count, int32_t scale,
+                    int32_t draw_health, uint8_t* rgb, void* stream) {
+  g_err.clear();
   if (!h || !rgb) return fail(WAB_E_INVALID, "wab_render: NULL argument");
   if (int rc = check_obs(obs, "wab_render")) return rc;
   if (scale < 1 || scale > 256) return fail(WAB_E_INVALID, "wab_render: scale must be in [1, 256]");
+  if (first < 0 || count < 0 || first > h->p.B || count > h->p.B - first)
+    return fail(WAB_E_INVALID, "wab_render_envs: [first, first + count) must lie in [0, B)");
   const Params& p = h->p;
   if ((uint64_t)p.W * scale * p.H * scale * 3 >= (1ull << 32))
     return fail(WAB_E_INVALID, "wab_render: image too large");
@@ -1004,26 +1013,26 @@ int wab_render(wab_handle* h, const wab_obs* obs, int32_t scale, int32_t draw_he
   rp.scale = scale;
   rp.restrict_view = p.restrict_view;
   rp.draw_health = draw_health != 0;
-  rp.B = p.B;
+  rp.B = count;
   std::memcpy(rp.mask_rows, p.mask_rows, sizeof(rp.mask_rows));
-  rp.planes = obs->planes;
-  rp.food_turns = obs->food_turns;
-  rp.role = obs->role;
-  rp.status = obs->status;
+  rp.planes = obs->planes + (size_t)first * p.OB;
+  rp.food_turns = obs->food_turns + first;
+  rp.role = obs->role + first;
+  rp.status = obs->status + first;
   rp.rgb = rgb;
-  if (p.B == 0) return WAB_OK;
+  if (count == 0) return WAB_OK;
   const uint64_t per_env = (uint64_t)p.W * scale * p.H * scale * 3;
   const uint64_t words = (per_env + 3) / 4;
   const unsigned gx = (unsigned)std::min<uint64_t>((words + 255) / 256, 1024);
   DeviceGuard guard(h->device);
-  for (int64_t e0 = 0; e0 < p.B; e0 += 65535) {  // grid.y is at most 65535 envs per launch
+  for (int64_t e0 = 0; e0 < count; e0 += 65535) {  // grid.y is at most 65535 envs per launch
     wab::RenderParams r2 = rp;
     r2.planes = rp.planes + (size_t)e0 * p.OB;
     r2.food_turns = rp.food_turns + e0;
     r2.role = rp.role + e0;
     r2.status = rp.status + e0;
     r2.rgb = rp.rgb + (size_t)e0 * per_env;
-    r2.B = std::min<int64_t>(65535, p.B - e0);
+    r2.B = std::min<int64_t>(65535, count - e0);
     hipLaunchKernelGGL(wab::wab_render_kernel, dim3(gx, (unsigned)r2.B), dim3(256), 0, (hipStream_t)stream, r2);
   }
   HIP_TRY(hipGetLastError());

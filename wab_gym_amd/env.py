@@ -237,6 +237,12 @@ class BatchedWolvesAndBushesEnv:
         """Synchronise; raise for timed-out hand-offs and deferred out-of-range actions."""
         self.counters()
 
+    @property
+    def terminal_observation(self):
+        """The last step's own observation buffer (dict of planes and scalars, for render(obs=)),
+        or None unless the env was made with return_terminal=True."""
+        return self._term
+
     def step(self, actions):
         """Advance every env one step (wab_env.py:250-342).  The returned obs, reward and done
         are views of the env's buffers, overwritten by the next step (clone to keep them)."""
@@ -357,16 +363,20 @@ class BatchedWolvesAndBushesEnv:
         return {"features": features, "scalars": scal.permute(1, 0, 2), "reward": rew, "done": done,
                 "returns": ret, "planes": planes}
 
-    def render(self, mode="rgb_array", scale=32, draw_health=True, out=None, obs=None):
+    def render(self, mode="rgb_array", scale=32, draw_health=True, out=None, obs=None, envs=None):
         """render (wab_env.py:468-502) of every env's current observation (or of `obs`, a
         dict of planes [B,3,W,S] and scalars [3,B] u8 tensors) on device: u8 [B, W*scale,
         H*scale, 3].  draw_health (the reference's default) draws the turns-until-starve
         count in blue at (0, 0) with PIL's default font's digit glyphs (tools/make_glyphs.py;
-        parity with the reference's pinned Pillow 7.2 font is unpinned)."""
+        parity with the reference's pinned Pillow 7.2 font is unpinned).  envs=(first, count)
+        renders only those envs: [count, W*scale, H*scale, 3]."""
         if mode != "rgb_array":
             raise NotImplementedError("only mode='rgb_array' (wab_env.py:104 metadata)")
         t = self._torch
-        shape = (self.num_envs, self.W * scale, self.H * scale, 3)
+        first, count = (0, self.num_envs) if envs is None else (int(envs[0]), int(envs[1]))
+        if first < 0 or count < 0 or first + count > self.num_envs:
+            raise ValueError("envs=(first, count) must lie in [0, %d)" % self.num_envs)
+        shape = (count, self.W * scale, self.H * scale, 3)
         img = t.empty(shape, dtype=t.uint8, device=self.device) if out is None else out
         if tuple(img.shape) != shape or img.dtype != t.uint8 or not img.is_contiguous() or img.device != self.device:
             raise ValueError("out must be a contiguous uint8 tensor of shape %s on %s" % (shape, self.device))
@@ -376,8 +386,9 @@ class BatchedWolvesAndBushesEnv:
             st = self._obs["struct"]
         else:
             st, keep = self._obs_struct(obs)
-        _lib.check(_lib.load().wab_render(self._h, ctypes.addressof(st), int(scale), int(bool(draw_health)),
-                                          img.data_ptr(), self._stream()), "wab_render")
+        _lib.check(_lib.load().wab_render_envs(self._h, ctypes.addressof(st), first, count, int(scale),
+                                               int(bool(draw_health)), img.data_ptr(), self._stream()),
+                   "wab_render_envs")
         del keep
         return img
 
