@@ -294,8 +294,13 @@ def test_monitor_video_over_device_env(tmp_path):
     assert sum(dones) >= 9  # episodes 0, 1 and 8 closed
     got = {}
     for v, m in env.videos:
-        with Image.open(v) as im:
-            got[json.load(open(m))["episode_id"]] = [np.asarray(f.convert("RGB")) for f in ImageSequence.Iterator(im)]
+        meta = json.load(open(m))
+        fr = []
+        with Image.open(v) as im:  # (PIL merges identical consecutive frames, adding their durations)
+            for f in ImageSequence.Iterator(im):
+                fr += [np.asarray(f.convert("RGB"))] * int(round(f.info["duration"] / (1000 / 12)))
+        assert len(fr) == meta["frames"]
+        got[meta["episode_id"]] = fr
     assert sorted(got) == [k for k in (0, 1, 8, 27, 64) if k < ep or k == ep]
     for k, fr in got.items():
         exp = want.get(k, cur)
