@@ -58,7 +58,7 @@ def main():
     L = _lib.load()
     L.wab_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     nb = (B + 63) // 64
-    st = torch.zeros((nb, 40), dtype=torch.int64, device="cuda:0")
+    st = torch.zeros((nb, 48), dtype=torch.int64, device="cuda:0")
     env.reset()
     L.wab_debug_set_stamps(env._h, st.data_ptr())
     g = torch.Generator(device="cuda:0")
@@ -182,7 +182,7 @@ def b2b_report(env, L, g, steps, n, graph=False):
 
     B = env.num_envs
     nb = (B + 63) // 64
-    bufs = [torch.zeros((nb, 40), dtype=torch.int64, device="cuda:0") for _ in range(2)]
+    bufs = [torch.zeros((nb, 48), dtype=torch.int64, device="cuda:0") for _ in range(2)]
     ends_cols = [6, 15, 21, 27] if env.step_kernel == "small" else [6, 14, 22, 30]
     acts = torch.randint(0, env.n_actions, (n, B), device="cuda:0", generator=g).to(torch.int8)
     entry, endx, lastx, gaps, spans, karg = [], [], [], [], [], []
@@ -269,6 +269,7 @@ def rollout_wide_report(env, st, g, launches, T):
         xcc = s[:, 33]
         acc.setdefault("xcd", []).append([(ex - ent)[xcc == x].mean() if (xcc == x).any() else 0.0 for x in range(8)])
         acc.setdefault("quart", []).append([q.mean() for q in np.array_split(ex - ent, 8)])
+        acc.setdefault("cores", []).append(coresidency(s, ent, ex))
         acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean(), np.percentile(ent - ent.min(), 99),
                                              np.percentile(ex - ent.min(), 1), np.percentile(ex - ent.min(), 50)))
     for k in seqs:
@@ -279,8 +280,41 @@ def rollout_wide_report(env, st, g, launches, T):
     la = np.mean(acc["launch"], axis=0) * 10 / 1000
     print("workgroup entry -> exit by XCD (us):", np.round(np.mean(acc["xcd"], axis=0) * 10 / 1000, 1))
     print("workgroup entry -> exit by blockIdx eighth (us):", np.round(np.mean(acc["quart"], axis=0) * 10 / 1000, 1))
+    print_coresidency(acc["cores"])
     print("launch: first entry -> last exit %.1f us (%.2f us per step); workgroup entry -> exit mean %.1f us; "
           "entries p99 %.1f us after the first; exits p1 %.1f, p50 %.1f us" % (la[0], la[0] / T, la[1], la[2], la[3], la[4]))
+
+
+def coresidency(s, ent, ex):
+    """Per launch, from the waves' HW_ID (slots 40..43) and the XCD (33): the workgroups of
+    each CU ranked by entry (dispatch order); returns durations by rank, by how many other
+    groups' W0 share this group's W0 SIMD (0..3), and the SIMD offsets of W1..W3 from W0."""
+    import numpy as np
+
+    hw = s[:, 40:44]
+    simd = (hw >> 4) & 3
+    key = (s[:, 33] << 8) | ((hw[:, 0] >> 8) & 0xFF)
+    dur = ex - ent
+    by_rank, by_share = [[] for _ in range(8)], [[] for _ in range(4)]
+    for k in np.unique(key):
+        idx = np.nonzero(key == k)[0]
+        idx = idx[np.argsort(ent[idx], kind="stable")]
+        for r, i in enumerate(idx[:8]):
+            by_rank[r].append(dur[i])
+            by_share[min(3, int((simd[idx, 0] == simd[i, 0]).sum()) - 1)].append(dur[i])
+    offs = np.bincount(((simd[:, 1:] - simd[:, :1]) % 4).ravel(), minlength=4)
+    return ([np.mean(v) if v else 0.0 for v in by_rank], [np.mean(v) if v else 0.0 for v in by_share],
+            [len(v) for v in by_share], offs, np.bincount(np.bincount(np.unique(key, return_inverse=True)[1])))
+
+
+def print_coresidency(rows):
+    import numpy as np
+
+    print("workgroup entry -> exit by dispatch rank on its CU (us):",
+          np.round(np.mean([r[0] for r in rows], axis=0) * 10 / 1000, 1))
+    print("  ... by other groups' W0 on its W0's SIMD (0..3):", np.round(np.mean([r[1] for r in rows], axis=0) * 10 / 1000, 1),
+          "counts", rows[-1][2])
+    print("  W1..W3 SIMD offset from W0 (0..3):", rows[-1][3], "; groups per CU histogram:", rows[-1][4])
 
 
 def rollout_report(env, st, g, launches, T, features=False):
@@ -324,7 +358,9 @@ def rollout_report(env, st, g, launches, T, features=False):
         ent, ex, xcc = s[:, 32], s[:, 39], s[:, 33]
         acc.setdefault("xcd", []).append([(ex - ent)[xcc == x].mean() if (xcc == x).any() else 0.0 for x in range(8)])
         acc.setdefault("eighth", []).append([q.mean() for q in np.array_split(ex - ent, 8)])
-        acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean()))
+        acc.setdefault("cores", []).append(coresidency(s, ent, ex))
+        acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean(), np.percentile(ent - ent.min(), 99),
+                                             np.percentile(ex - ent.min(), 1), np.percentile(ex - ent.min(), 50)))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
@@ -333,10 +369,11 @@ def rollout_report(env, st, g, launches, T, features=False):
     print("W0: loop top -> its start (parameters, slices) %.2f us; step start -> past its end barrier %.2f us"
           % (lp[0], lp[1]))
     la = np.mean(acc["launch"], axis=0) * 10 / 1000
-    print("launch: first entry -> last exit %.1f us (%.2f us per step); workgroup entry -> exit mean %.1f us"
-          % (la[0], la[0] / T, la[1]))
+    print("launch: first entry -> last exit %.1f us (%.2f us per step); workgroup entry -> exit mean %.1f us; "
+          "entries p99 %.1f us after the first; exits p1 %.1f, p50 %.1f us" % (la[0], la[0] / T, la[1], la[2], la[3], la[4]))
     print("workgroup entry -> exit by XCD (us):", np.round(np.mean(acc["xcd"], axis=0) * 10 / 1000, 1))
     print("workgroup entry -> exit by blockIdx eighth (us):", np.round(np.mean(acc["eighth"], axis=0) * 10 / 1000, 1))
+    print_coresidency(acc["cores"])
     if features:
         f = np.mean(acc["feat"], axis=0) * 10 / 1000
         print("features: emitted %.2f, wave 0's row stores issued %.2f us" % (f[0], f[1]))

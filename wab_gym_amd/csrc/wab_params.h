@@ -45,6 +45,9 @@ __host__ __device__ inline uint32_t xy_pack(int32_t x, int32_t y) {
 __host__ __device__ inline int32_t xy_x(uint32_t p) { return (int32_t)(int16_t)(p & 0xFFFFu); }
 __host__ __device__ inline int32_t xy_y(uint32_t p) { return (int32_t)(int16_t)(p >> 16); }
 
+// diagnostic builds (-DWAB_STAMPS): int64 stamps per workgroup (tools/phase_stamps.py)
+constexpr int kStampStride = 48;
+
 struct Params {
   // ---- geometry
   int32_t W, H, S;          // viewport width (axis 0), height (axis 1), row stride in bytes

@@ -62,7 +62,7 @@ __device__ __forceinline__ void bitmap_to_plane(const Params& p, uint32_t* bm, i
 #define WAB_STAMP(slot)                                                                    \
   do {                                                                                     \
     if (threadIdx.x == 0 && p.stamps)                                                      \
-      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();         \
+      p.stamps[(size_t)blockIdx.x * kStampStride + (slot)] = __builtin_amdgcn_s_memrealtime();         \
   } while (0)
 #else
 #define WAB_STAMP(slot) do {} while (0)

@@ -39,14 +39,14 @@
 namespace wab {
 
 // Diagnostic build (-DWAB_STAMPS): lane 0 of each wave records s_memrealtime (100 MHz) at
-// phase boundaries into p.stamps[workgroup * 40 + slot] (W0 0..9, W1 10..15, W2 16..21, W3 22..27):
+// phase boundaries into p.stamps[workgroup * kStampStride + slot] (W0 0..9, W1 10..15, W2 16..21, W3 22..27):
 // a wave's stamps k, k+1, k+2, k+3 close its phases P0..P3 (the barrier waits sit at the
 // start of the next phase), the last one the retirement of its obs stores.
 #ifdef WAB_STAMPS
 #define SMALL_STAMP(slot)                                                                \
   do {                                                                                   \
     if (lane == 0 && p.stamps && (!ROLL || t == p.n_steps / 2))                          \
-      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+      p.stamps[(size_t)blockIdx.x * kStampStride + (slot)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 #else
 #define SMALL_STAMP(slot) do {} while (0)
@@ -1342,7 +1342,7 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if ((tid & 63) == 0 && p.stamps) {
     const int slot[4] = {6, 15, 21, 27};
-    p.stamps[(size_t)blockIdx.x * 40 + slot[tid >> 6]] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(size_t)blockIdx.x * kStampStride + slot[tid >> 6]] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
@@ -1380,7 +1380,7 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
 #ifdef WAB_STAMPS
   const auto stamp = [&](int slot) {  // (multi-step launches: the middle step, wave 0)
     if (ROLL && threadIdx.x == 0 && p.stamps && t == p.n_steps / 2)
-      p.stamps[(size_t)blockIdx.x * 40 + slot] = __builtin_amdgcn_s_memrealtime();
+      p.stamps[(size_t)blockIdx.x * kStampStride + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(36);  // the feature bits emitted
 #endif
@@ -1445,12 +1445,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
   if (threadIdx.x == 0 && p0.stamps) {  // kernel entry (slot 32), the XCD (33), first kernarg field in (34)
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    p0.stamps[(size_t)blockIdx.x * 40 + 34] = __builtin_amdgcn_s_memrealtime();
-    p0.stamps[(size_t)blockIdx.x * 40 + 32] = t_entry;
-    p0.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 34] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 32] = t_entry;
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 33] = xcc & 0xFu;
   }
 #endif
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (uniform branches)
+#ifdef WAB_STAMPS
+  if (lane == 0 && p0.stamps) {  // each wave's HW_ID (SIMD, CU, SE) in slots 40..43
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 40 + wave] = hw;
+  }
+#endif
 #ifdef WAB_ONLY_WAVE  // static per-wave instruction counts (tools/isa_count.py); not a runnable build
   if (wave != WAB_ONLY_WAVE) return;
 #endif
@@ -1487,7 +1494,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
 #define ROLL_LOOP_STAMP(slot, cond)                                                          \
   do {                                                                                       \
     if (threadIdx.x == 0 && p0.stamps && (cond))                                             \
-      p0.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();         \
+      p0.stamps[(size_t)blockIdx.x * kStampStride + (slot)] = __builtin_amdgcn_s_memrealtime();         \
   } while (0)
 #else
 #define ROLL_LOOP_STAMP(slot, cond) do {} while (0)
@@ -1546,7 +1553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && p0.stamps)  // every store of the workgroup retired (slot 39)
-      p0.stamps[(size_t)blockIdx.x * 40 + 39] = __builtin_amdgcn_s_memrealtime();
+      p0.stamps[(size_t)blockIdx.x * kStampStride + 39] = __builtin_amdgcn_s_memrealtime();
 #endif
   }
 }

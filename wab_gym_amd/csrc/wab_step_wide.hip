@@ -40,7 +40,7 @@ namespace wab {
 #define WIDE_STAMP(slot)                                                                 \
   do {                                                                                   \
     if (lane == 0 && p.stamps)                                                           \
-      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+      p.stamps[(size_t)blockIdx.x * kStampStride + (slot)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 #else
 #define WIDE_STAMP(slot) do {} while (0)
@@ -293,8 +293,8 @@ __global__ __launch_bounds__(256) void wab_step_wide(Params p0) {
   if (threadIdx.x == 0 && p.stamps) {  // kernel entry (slot 32) and the XCD (slot 33)
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    p.stamps[(size_t)blockIdx.x * 40 + 32] = __builtin_amdgcn_s_memrealtime();
-    p.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
+    p.stamps[(size_t)blockIdx.x * kStampStride + 32] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(size_t)blockIdx.x * kStampStride + 33] = xcc & 0xFu;
   }
 #endif
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -951,6 +951,7 @@ struct RowQueue {
   uint8_t* out;
   unsigned long long jm;
   bool untouched_only;
+  bool skip_p2;  // the ostrich plane's whole lines are stored by drain_plane2
 };
 __device__ __forceinline__ RowQueue row_queue(const Params& p, uint32_t* ctr, uint32_t n_rows, const uint32_t* bm,
                                               const uint32_t* wp, uint8_t* out) {
@@ -965,6 +966,7 @@ __device__ __forceinline__ RowQueue row_queue(const Params& p, uint32_t* ctr, ui
   q.out = out;
   q.jm = 0ull;
   q.untouched_only = false;
+  q.skip_p2 = false;
   return q;
 }
 template <bool IF>
@@ -1013,6 +1015,7 @@ __device__ __forceinline__ RowQueue untouched_rows(const Params& p, uint32_t* ct
   RowQueue q = row_queue(p, ctr, n_rows, bm, wp, out);
   q.jm = (unsigned long long)blk[1] | ((unsigned long long)blk[2] << 32);
   q.untouched_only = true;
+  q.skip_p2 = true;
   return q;
 }
 
@@ -1027,6 +1030,10 @@ __device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, 
   const uint32_t ch = 64u * b + (uint32_t)lane, row = CPR == 2u ? ch >> 1 : ch, half = CPR == 2u ? ch & 1u : 0u;
   if (row >= q.n_rows) return;
   const uint32_t e = __umulhi(row, q.magic), rr = row - e * 3u * W;
+  if (q.skip_p2) {  // (a whole line inside the env's ostrich plane: stored already)
+    const int o0 = (int)(((64u * b + (uint32_t)lane) & ~7u) - e * CPE), p2 = (int)(2u * W * CPR);
+    if (o0 >= p2 && o0 + 8 <= (int)(3u * W * CPR)) return;
+  }
   if (IF) {  // (only the lines that touch no done env)
     const unsigned long long jn = q.jm | (q.jm << 1) | (q.jm >> 1);
     if ((jn >> e) & 1ull) {
@@ -1041,6 +1048,32 @@ __device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, 
   __builtin_nontemporal_store(expand16((v >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(q.out) + e * CPE + rr * CPR + half);
 }
 
+// The last step's ostrich-plane lines: the plane is the centre cell alone, the same in every
+// observation (a done env's new episode included), so its whole lines (inside one env's plane
+// 2) can go out from the step's start, under the step's compute; one env per claimed block,
+// 6-7 lines per instruction.  Claimed from ctr until the envs run out (true) or flag >= v
+// (false).  (Measured, B = 65536: one-step launches into a 32-slot ring 59.1 -> 52.3 us; the
+// same gated until W0's and W1's step-0 loads were in: 53.0; 64-step launches: unchanged.)
+__device__ __forceinline__ bool drain_plane2(const Params& p, uint32_t* ctr, int n_active, uint8_t* out, int lane,
+                                             const uint32_t* flag = nullptr, uint32_t v = 0u) {
+  const uint32_t CPE = (uint32_t)p.OB >> 4, CPR = (uint32_t)p.S >> 4, W = (uint32_t)p.W;
+  while (true) {
+    if (v && __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= v)
+      return false;
+    uint32_t e = 0;
+    if (lane == 0) e = atomicAdd(ctr, 1u);
+    e = (uint32_t)__shfl((int)e, 0);
+    if (e >= (uint32_t)n_active) return true;
+    const uint32_t base = e * CPE, a = (base + 2u * W * CPR + 7u) & ~7u, z = (base + 3u * W * CPR) & ~7u;
+    const uint32_t ch = a + (uint32_t)lane;  // (z - a <= W * CPR <= 64)
+    if (ch < z) {
+      const uint32_t o = ch - base, rr = CPR == 2u ? o >> 1 : o, half = CPR == 2u ? o & 1u : 0u;
+      const uint32_t v2 = rr - 2u * W == (uint32_t)p.cw ? 1u << p.ch : 0u;
+      __builtin_nontemporal_store(expand16((v2 >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(out) + ch);
+    }
+  }
+}
+
 // Diagnostic build (-DWAB_STAMPS): the middle step's phase stamps of the rollout build
 // (tools/phase_stamps.py --rollout T --config wide31): W0 0..7, W1 8..13, W2 16..20, W3 24..27,
 // the done-env section 36..39
@@ -1048,7 +1081,7 @@ __device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, 
 #define ROLLW_STAMP(slot)                                                                \
   do {                                                                                   \
     if (lane == 0 && p.stamps && t == T / 2)                                             \
-      p.stamps[(size_t)blockIdx.x * 40 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+      p.stamps[(size_t)blockIdx.x * kStampStride + (slot)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 #else
 #define ROLLW_STAMP(slot) do {} while (0)
@@ -1084,8 +1117,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   if (tid == 0 && p0.stamps) {  // kernel entry (slot 32), the XCD (33)
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    p0.stamps[(size_t)blockIdx.x * 40 + 32] = __builtin_amdgcn_s_memrealtime();
-    p0.stamps[(size_t)blockIdx.x * 40 + 33] = xcc & 0xFu;
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 32] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 33] = xcc & 0xFu;
+  }
+  if (lane == 0 && p0.stamps) {  // each wave's HW_ID (SIMD, CU, SE) in slots 40..43
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 40 + wave] = hw;
   }
 #endif
   const int n_active = (int)min((int64_t)64, p0.B - g0);
@@ -1112,7 +1150,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   for (int t = 0; t < T; ++t) {
 #ifdef WAB_STAMPS
     if (tid == 0 && p0.stamps && t == T / 2)  // the middle step's loop top
-      p0.stamps[(size_t)blockIdx.x * 40 + 35] = __builtin_amdgcn_s_memrealtime();
+      p0.stamps[(size_t)blockIdx.x * kStampStride + 35] = __builtin_amdgcn_s_memrealtime();
 #endif
     const bool last = t == T - 1;
     const int cur = t & 1;
@@ -1562,7 +1600,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       ROLLW_STAMP(10);
       lds_barrier();  // B1
       ROLLW_STAMP(11);
-      if (t > 0) drain_rows(p, qp, lane, flag + 2, at_b2);  // (idle until B2: store)
+      {
+        const bool rest = t > 0 ? drain_rows(p, qp, lane, flag + 2, at_b2) : true;  // (idle until B2: store)
+        if (last && rest) drain_plane2(p, flag + 6, n_active, out, lane, flag + 2, at_b2);
+      }
       lds_barrier();  // B2
       ROLLW_STAMP(12);
     } else {
@@ -1574,6 +1615,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       // launch's tail alone (group durations by dispatch quarter 1720, 1930, 2170, 2440 us;
       // rotating: 1965, 2070, 2174, 2304).  C3 T = 64: 2728-2737 -> 2618-2628 us per launch
       // (tools/ab_wide.sh; every wave rotating: 2609-2633; static inverse-age priority 2786).
+      // (one-step launches: priority = age, the youngest first; 59.1 us per step into a ring,
+      // against 63.2 at priority 0 and 63.5 oldest first)
       set_prio_dyn(((blockIdx.x >> 8) + (uint32_t)t) & 3u);
       if (wave == 2 && t == 0) {
         copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);
@@ -1583,14 +1626,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
         if (lane == 0) lds_publish_step(flag + 1, 1u);  // (W0 waits for the tables once)
       }
       ROLLW_STAMP(8 * wave + 1);
-      if (t > 0) drain_rows(p, qp, lane, flag + 2, at_b1);  // step t - 1's rows until W0 reaches B1
+      {
+        const bool rest = t > 0 ? drain_rows(p, qp, lane, flag + 2, at_b1) : true;  // step t - 1's rows until W0 reaches B1
+        if (last && rest) drain_plane2(p, flag + 6, n_active, out, lane, flag + 2, at_b1);
+      }
       ROLLW_STAMP(8 * wave + 2);
       lds_barrier();  // B1
       if (wave == 3 && !last) wide_prefetch_actions(p, act, lane);  // (read after this step's end)
-      if (t > 0) drain_rows(p, qp, lane, flag + 2, at_b2);  // ... until W0 reaches B2
+      {
+        const bool rest = t > 0 ? drain_rows(p, qp, lane, flag + 2, at_b2) : true;  // ... until W0 reaches B2
+        if (last && rest) drain_plane2(p, flag + 6, n_active, out, lane, flag + 2, at_b2);
+      }
       ROLLW_STAMP(8 * wave + 3);
       lds_barrier();  // B2
       if (t > 0) drain_rows(p, qp, lane);  // ... the rest, while W0 and W1 build the new episodes
+      if (last) drain_plane2(p, flag + 6, n_active, out, lane);
       if (last) drain_rows(p, untouched_rows(p, flag + 4 + cur, n_rows, bm, wp, out, blk), lane);
       ROLLW_STAMP(8 * wave + 4);
     }
@@ -1682,6 +1732,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     }
     if (wave < 2) {  // W0 and W1 are done with the step: they store too
       if (t > 0) drain_rows(p, qp, lane);
+      if (last) drain_plane2(p, flag + 6, n_active, out, lane);
       if (last) drain_rows(p, untouched_rows(p, flag + 4 + cur, n_rows, bm, wp, out, blk), lane);
     }
     if (wave == 0) ROLLW_STAMP(39);
@@ -1689,7 +1740,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     lds_barrier();  // the step's end: its obs buffers are complete; the next step's inputs are in
 #ifdef WAB_STAMPS
     if (tid == 0 && p0.stamps && t == T / 2)  // past the middle step's end barrier
-      p0.stamps[(size_t)blockIdx.x * 40 + 38] = __builtin_amdgcn_s_memrealtime();
+      p0.stamps[(size_t)blockIdx.x * kStampStride + 38] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (last) {
       // the last step's obs lines that touch a done env (its new episode, its neighbours' S), by
@@ -1711,7 +1762,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0 && p0.stamps)  // every store of the workgroup retired (slot 34)
-    p0.stamps[(size_t)blockIdx.x * 40 + 34] = __builtin_amdgcn_s_memrealtime();
+    p0.stamps[(size_t)blockIdx.x * kStampStride + 34] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
