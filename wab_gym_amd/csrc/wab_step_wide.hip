@@ -1196,6 +1196,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
           hdr = p.hdr[g];
           a = (int)p.actions[g];
         }
+        if (wave == 1) {  // W1: the thresholds and bitmap rows in the same round trip (one-step launches
+                          // into a ring: B1 at 12.9 -> 10.6 us, 52.35 -> 52.1 us per launch)
+          const int nthr = p.max_berries;
+          uint64_t tv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
+          const uint4* sp = reinterpret_cast<const uint4*>(p.bushmap + (size_t)(active ? g : 0) * 32u);
+          uint4 v[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = sp[k];
+          __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t r[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (4 * k + q < p.W) bm_prev[me + (uint32_t)(4 * k + q)] = r[q];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
+          if (lane == 0) bush_thr_pads(thr, nthr);
+        }
         // (every step-0 load settled inside its branch: the waitcnt pass would otherwise put
         // vmcnt(0) waits at the join that every later step executes too, each one waiting for all
         // of the wave's obs stores in flight)
@@ -1524,29 +1547,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     } else if (wave == 1) {
       // ---------------------------------------------- W1 P0: the view bitmap
       __builtin_amdgcn_s_setprio(2);
-      // source: the last step's bitmaps (step 0: the state's, loaded into that buffer)
+      // source: the last step's bitmaps (step 0: the state's, loaded with the header)
       uint32_t* src = bm_prev;
-      if (t == 0) {
-        const int nthr = p.max_berries;
-        uint64_t tv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) tv[k] = nthr > 0 ? p.thresholds[min(64 * k + lane, nthr - 1)] : 0ull;
-        const int64_t ga = active ? g : 0;
-        const uint4* sp = reinterpret_cast<const uint4*>(p.bushmap + (size_t)ga * 32u);
-#pragma unroll 1
-        for (int k = 0; k < 8; k += 2) {  // (step 0 only)
-          const uint4 v0 = sp[k], v1 = sp[k + 1];
-          const uint32_t r[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (4 * k + q < p.W) src[me + (uint32_t)(4 * k + q)] = r[q];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (64 * k + lane < nthr) thr[64 * k + lane] = tv[k];
-        if (lane == 0) bush_thr_pads(thr, nthr);
-        __builtin_amdgcn_s_waitcnt(0);
-      }
       // the last step's eaten-empty centre tile of a continuing env (its obs were pre-eat S),
       // applied to the source's centre row as it is read
       bool eaten_empty = false;
