@@ -315,6 +315,20 @@ __device__ __forceinline__ bool info_starved(uint32_t v) { return (v & 1u) != 0u
 // sets' gap thresholds evaluated without a table (binary powering from 16 doubles in the kernel
 // arguments: 11.1 us, more SGPR spills; from device memory: 14.0 us).
 constexpr int kW1ResetPrio = 2;
+
+// A wave's issue priority `level` (0..3, by its role).  In a wab_rollout_features launch
+// (`rot`) the levels fold to two (0, 1) and a boost of 2 alternates step by step between the
+// co-resident workgroups of a CU (blockIdx b, b + 256, ...: at equal priority the arbiter
+// favours the oldest): C5 T = 64 23.84-23.87 -> 23.36-23.37 us per step; the plain rollout
+// measured slower with it (5.70-5.75 -> 5.93-5.94), and with the four levels rotating, role
+// ignored (C5 23.74-23.75, default 5.95-5.97).
+template <bool ROLL>
+__device__ __forceinline__ void role_prio(uint32_t level, int t, bool rot) {
+  if (ROLL && rot)
+    set_prio_dyn((level >= 2u ? 1u : 0u) + 2u * (((blockIdx.x >> 8) + (uint32_t)t) & 1u));
+  else
+    set_prio_dyn(level);
+}
 // the entering strip's cells are drawn in two parts, [0, kStripW1) on W1 after the tile value
 // and the rest on W3 after the spawn set
 constexpr int kStripW1 = 8;
@@ -777,7 +791,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   s.info[lane] = (starved ? 1u : 0u) | ((uint32_t)role << 8) | ((uint32_t)ne << 16) | ((uint32_t)ndep << 24);
   SMALL_STAMP(3);
   lds_barrier();  // B1: kill flags in; starve flags, bush grid and counts out
-  __builtin_amdgcn_s_setprio(1);
+  role_prio<ROLL>(1, t, p.features != nullptr);
 
   // status (starve overrides kill), reward/done (:328-340), scalars, bushes and food
   const bool killed = s.kill[lane] != 0u;
@@ -897,7 +911,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(10);
-  __builtin_amdgcn_s_setprio(2);  // the tile value is on the bushes wave's path
+  role_prio<ROLL>(2, t, p.features != nullptr);  // the tile value is on the bushes wave's path
   HeadRaw hr;
   if (ROLL && t > 0) {  // (multi-step launch: the thresholds are in LDS since step 0)
     hr.hdr = carry->hdr;
@@ -928,7 +942,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   s.cval[lane] =
       (uint32_t)bush_value_fast(s.thr, p.max_berries, draw_U(h.cpos, make_ts(SITE_BUSH, 0, 0), b0, b1), p.bush_power);
   lds_publish(s.flag);  // every lane: each orders its own cval entry
-  __builtin_amdgcn_s_setprio(0);
+  role_prio<ROLL>(0, t, p.features != nullptr);
   if (p.features && !p.restrict_view && !ROLL)  // rows 0..31 (step_features)
     early_view_zeros(p, 0u, (uint32_t)min((int64_t)32, p.B - (int64_t)blockIdx.x * 64), lane);
   SMALL_STAMP(11);
@@ -944,7 +958,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   if (jm) {
     // (W3 waits for these draws before it builds the new episodes: W1 at issue priority 2
     // while it makes them, multi-step launches: 6.41 -> 6.33 us per step, profiles/r03_ab2/)
-    if (ROLL) __builtin_amdgcn_s_setprio(kW1ResetPrio);
+    if (ROLL) role_prio<ROLL>(kW1ResetPrio, t, p.features != nullptr);
     if (job) {
       const uint64_t ek2 = mix64(h.kenv ^ (uint64_t)(h.hdr.w + 1u));  // the new episode's key
       const int j = __popcll(jm & ((1ull << lane) - 1ull));
@@ -952,7 +966,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     }
     reset_chunk(p, s.tiles, s.jkey, __popcll(jm), 0u, lane, s.jbm);
     lds_publish(&s.flag[1]);
-    if (ROLL) __builtin_amdgcn_s_setprio(0);
+    if (ROLL) role_prio<ROLL>(0, t, p.features != nullptr);
   }
   if (h.active && (!job || p.t_planes)) {
     // S of the continuing envs (and of the done ones when their terminal obs is asked for);
@@ -1169,7 +1183,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   const Lds s = lds_of(lds, L);
   const int64_t g = (int64_t)blockIdx.x * 64 + lane;
   SMALL_STAMP(22);
-  if (ROLL) __builtin_amdgcn_s_setprio(0);  // (raised after B1 of the last step)
+  if (ROLL) role_prio<ROLL>(0, t, p.features != nullptr);  // (raised after B1 of the last step)
   HeadRaw hr;
   if (ROLL && t > 0) {  // (multi-step launch: the tables are in LDS since step 0)
     hr.hdr = carry->hdr;
@@ -1225,7 +1239,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   s.strip[64 + lane] = strip_draws(p, h, b0, b1, kStripW1, 1 << 30);  // the entering strip, part 2
   SMALL_STAMP(23);
   lds_barrier();  // B1
-  __builtin_amdgcn_s_setprio(3);
+  role_prio<ROLL>(3, t, p.features != nullptr);
   // reset draws of every done env (generate_bushes, initialize_wolves), all view cells, then
   // (unless the terminal obs is asked for: W0 after B2) the new episodes themselves
   const bool job = h.active && p.autoreset && env_done(p, h, info_starved(s.info[lane]), s.kill[lane] != 0u);
@@ -1533,9 +1547,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     if (wave == 0) {
       CarryW0 c;
       WAB_ROLL_STEP({
-        __builtin_amdgcn_s_setprio(3);
+        role_prio<true>(3, t, p.features != nullptr);
         bushes_wave<SLOTS, G, true>(p, L, lds, lane, &c, t, t == T - 1);
-        __builtin_amdgcn_s_setprio(0);
+        role_prio<true>(0, t, p.features != nullptr);
       })
     } else if (wave == 1) {
       CarryPtr<CarryHdr> c;
