@@ -686,8 +686,8 @@ int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* re
     // step).  Into the buffer of the last step (the env's own, rewritten every step, which the
     // 256 MB Infinity Cache holds) the per-step kernel, which stores each plane as soon as it is
     // final (a line at a plane or env boundary in two parts, merged on die).  Measured at
-    // B = 65536 (C3): into a 32-slot ring 62.8 against 73.1 us, into one buffer 62.5 against
-    // 45.9 us.  The results are the same either way.
+    // B = 65536 (C3): into a 32-slot ring 52.0 against 73.1 us (round 3's per-step kernel), into
+    // one buffer 62.5 against 45.9 us.  The results are the same either way.
     if (h->n_blocks == 0) return WAB_OK;
     p.n_steps = 1;
     hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_roll_lds_bytes,

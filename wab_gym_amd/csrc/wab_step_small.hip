@@ -814,7 +814,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
     uint8_t* fts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_food_turns, (uint64_t)p.food_turns));
     uint8_t* rls = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_role, (uint64_t)p.role));
     uint8_t* sts = reinterpret_cast<uint8_t*>(sel64(job, (uint64_t)p.t_status, (uint64_t)p.status));
-    if (!job || p.t_planes) {
+    if (!job || (!ROLL && p.t_planes)) {
       fts[g] = (uint8_t)ft;
       rls[g] = (uint8_t)role;
       sts[g] = (uint8_t)status;
@@ -839,7 +839,7 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, lane);
   SMALL_STAMP(4);
   lds_barrier();  // B2: S rendered (done envs too when their terminal obs is asked for)
-  if (p.t_planes) {
+  if (!ROLL && p.t_planes) {  // (terminal obs: per-step launches only)
     // terminal obs: the step's own obs of every done env (bytes); then its new episode
     unsigned long long wolf_of = 0;
     if (jm) {
@@ -968,7 +968,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
     lds_publish(&s.flag[1]);
     if (ROLL) role_prio<ROLL>(0, t, p.features != nullptr);
   }
-  if (h.active && (!job || p.t_planes)) {
+  if (h.active && (!job || (!ROLL && p.t_planes))) {
     // S of the continuing envs (and of the done ones when their terminal obs is asked for);
     // needed only at B2, so after the reset draws W3 waits for
     render_s(p, s, lane, info, h.dir);
@@ -978,7 +978,7 @@ __device__ __forceinline__ unsigned long long draws_wave(const Params& p, const 
   if (ROLL && !last) prefetch_actions(p, s, lane);
   SMALL_STAMP(13);
   lds_barrier();  // B2
-  if (p.t_planes) lds_barrier();  // B3
+  if (!ROLL && p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(14);
   if (ROLL && lane == 0) {  // every hand-off of this step is done: clear the flags for the next
     s.flag[0] = 0u;
@@ -1146,7 +1146,7 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   if (ROLL && carry->prev_stream) store_units_nt<128, 12>(p, carry->prev_planes, carry->prev_stream, 64 + lane);
   SMALL_STAMP(19);
   lds_barrier();  // B2
-  if (p.t_planes) lds_barrier();  // B3
+  if (!ROLL && p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(20);
   if (ROLL && !last) {  // the slots for the next step: a new episode's wolves from W3's cells
     if (job) {
@@ -1257,7 +1257,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
     for (uint32_t c0 = 64; c0 < (uint32_t)p.WH; c0 += 64)  // cells [0, 64): W1
       reset_chunk(p, s.tiles, jkey, n_jobs, c0, lane, s.jbm);
     SMALL_STAMP(24);
-    if (!p.t_planes) {
+    if (ROLL || !p.t_planes) {
       // the part of the new episode that needs only its key, while W1 may still be drawing
       unsigned long long wolf_of = 0;
       const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB;
@@ -1270,7 +1270,7 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   }
   SMALL_STAMP(25);
   lds_barrier();  // B2
-  if (p.t_planes) lds_barrier();  // B3
+  if (!ROLL && p.t_planes) lds_barrier();  // B3
   SMALL_STAMP(26);
   if (ROLL && !last) {
     const uint32_t status = info_starved(s.info[lane]) ? 1u : s.kill[lane] != 0u ? 2u : misc_status(h.hdr.z);
