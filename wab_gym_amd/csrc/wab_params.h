@@ -161,9 +161,13 @@ constexpr int kMaxFusedReturnSteps = 128;
 
 // LDS of the four-wave small-view step (wab_step_small.hip): one 64-env group per
 // workgroup (dwords)
+// the small kernel's multi-step launches keep eaten-log entries 0..3 of an env in W0's
+// registers and 4 .. kSmallLog - 1 in LDS; later ones stay in HBM
+constexpr int kSmallLog = 12;
 struct SmallLayout {
   uint32_t tiles, thr, gap, stream, stream_words, cval, flag, wolfp, kill, bushp, strip, gone, info, spawn, jbm, jkey;
   uint32_t carry, act;  // multi-step launches: the new episodes' state for the next step, its actions
+  uint32_t elog;        // multi-step launches: eaten-log entries 4 .. kSmallLog - 1 (xy dwords, then rem bytes)
   uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
   uint32_t rcode;       // wab_rollout_features with returns: [n_steps][64] reward codes (bytes)
@@ -190,6 +194,7 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.jkey = o; o += 2u * 2u * 64u;
   L.carry = o; o += 8u * 64u;  // per env: role | new wolves << 8, food (2), wolf cells (4), pad
   L.act = o; o += 16u;         // 64 int8 actions
+  L.elog = o; o += (uint32_t)(kSmallLog - 4) * 64u * 5u / 4u;
   L.stream2 = o; o += L.stream_words + 4u;
   L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads

@@ -276,6 +276,8 @@ struct Lds {
   uint32_t* carry;  // [64][8] multi-step launches: a new episode's role | wolves << 8, food, wolf cells (W3)
   uint32_t* act;    // [16] multi-step launches: the next step's 64 actions (W1)
   uint8_t* rcode;   // [n_steps][64] wab_rollout_features with returns: each step's reward code (W0)
+  uint32_t* elxy;   // [kSmallLog - 4][64] multi-step launches: eaten-log entries 4.. (W0)
+  uint8_t* elrem;   // [kSmallLog - 4][64]
 };
 
 __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
@@ -286,6 +288,8 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   s.stream = lds + L.stream;
   s.cval = lds + L.cval;
   s.flag = lds + L.flag;
+  s.elxy = lds + L.elog;
+  s.elrem = reinterpret_cast<uint8_t*>(lds + L.elog + (uint32_t)(kSmallLog - 4) * 64u);
   s.wolfp = reinterpret_cast<uint4*>(lds + L.wolfp);
   s.kill = lds + L.kill;
   s.bushp = reinterpret_cast<uint4*>(lds + L.bushp);
@@ -446,7 +450,7 @@ struct CarryW0 {
   uint4 hdr;
   double food;
   uint32_t bw[4];            // view bitmap (post-eat)
-  uint32_t lxy[4], lrem[4];  // eaten-log entries 0..3 (entries >= 4 stay in HBM)
+  uint32_t lxy[4], lrem[4];  // eaten-log entries 0..3 (4 .. kSmallLog - 1 in LDS, later ones in HBM)
 };
 template <int SLOTS>
 struct CarryW2 {
@@ -696,6 +700,14 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   }
   if (init) lds_barrier();  // B_init: the hand-off flags are clear
   int ne = (int)misc_ne(h.hdr.z), ndep = (int)misc_ndep(h.hdr.z);
+  if (ROLL && t == 0) {  // entries 4 .. kSmallLog - 1 into LDS, for the whole launch
+    for (int i = 4; i < kSmallLog; ++i)
+      if (active && i < ne && i < p.eaten_cap) {
+        s.elxy[(i - 4) * 64 + lane] = p.eaten_xy[(int64_t)i * p.B + g];
+        s.elrem[(i - 4) * 64 + lane] = p.eaten_rem[(int64_t)i * p.B + g];
+      }
+    __builtin_amdgcn_s_waitcnt(0);  // (settled inside the branch: no vmcnt wait at the join)
+  }
   const int status_old = (int)misc_status(h.hdr.z);
   const int role = h.role;
   M128 bm = m_make(bw0, bw1, bw2, bw3);  // scroll (generate_bushes keeps the tiles in view, :613-629)
@@ -725,7 +737,20 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
   bm = m_andn(bm, gone);
   bool center_bush = m_test(bm, ccb);
   if (ne > 4 && (center_bush || (ndep > 0 && h.dir != DIR_STAY))) {
-    for (int i0 = 4; i0 < ne; i0 += 4) {
+    // multi-step launches: entries 4 .. kSmallLog - 1 from LDS (a vector load here would wait
+    // for every obs store the wave has in flight), later ones from HBM
+    const int i_hbm = ROLL ? kSmallLog : 4;
+    if (ROLL)
+      for (int i0 = 4; i0 < ne && i0 < kSmallLog; i0 += 4) {
+        uint32_t exy[4], erem[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          exy[k] = s.elxy[(i0 + k - 4) * 64 + lane];
+          erem[k] = s.elrem[(i0 + k - 4) * 64 + lane];
+        }
+        scan_log(p, h, exy, erem, i0, ne, found, found_rem, gone);
+      }
+    for (int i0 = i_hbm; i0 < ne; i0 += 4) {
       uint32_t exy[4] = {0u, 0u, 0u, 0u}, erem[4] = {0u, 0u, 0u, 0u};  // (entries 0..3 stay in lxy, lrem)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -769,6 +794,12 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
           lxy[k] = h.cpos;
           lrem[k] = (uint32_t)(rem - 1);
         }
+      ne += 1;
+    } else if (ROLL && found >= 4 && found < kSmallLog) {  // (entries 4.. in LDS)
+      s.elrem[(found - 4) * 64 + lane] = (uint8_t)(rem - 1);
+    } else if (ROLL && found < 0 && ne >= 4 && ne < kSmallLog && ne < p.eaten_cap) {
+      s.elxy[(ne - 4) * 64 + lane] = h.cpos;
+      s.elrem[(ne - 4) * 64 + lane] = (uint8_t)(rem - 1);
       ne += 1;
     } else if (found >= 0) {
       p.eaten_rem[(int64_t)found * p.B + g] = (uint8_t)(rem - 1);
@@ -890,12 +921,17 @@ __device__ __forceinline__ unsigned long long bushes_wave(const Params& p, const
         carry->lxy[i] = lxy[i];
         carry->lrem[i] = lrem[i];
       }
-    } else if (active && !job) {  // the eaten-log entries kept in registers
+    } else if (active && !job) {  // the eaten-log entries kept in registers and LDS
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (i < ne && i < p.eaten_cap) {
           p.eaten_xy[(int64_t)i * p.B + g] = lxy[i];
           p.eaten_rem[(int64_t)i * p.B + g] = (uint8_t)lrem[i];
+        }
+      for (int i = 4; i < kSmallLog; ++i)
+        if (i < ne && i < p.eaten_cap) {
+          p.eaten_xy[(int64_t)i * p.B + g] = s.elxy[(i - 4) * 64 + lane];
+          p.eaten_rem[(int64_t)i * p.B + g] = s.elrem[(i - 4) * 64 + lane];
         }
     }
   }
