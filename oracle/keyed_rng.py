@@ -64,6 +64,20 @@ SITE_DESPAWN = 3
 SITE_START_FOOD = 4
 SITE_START_ROLE = 5
 SITE_GAP = 6
+# Environment 2.0 torus world (`Environment 2.0/WAB_Environment2.py`, `World.py`): its draws are
+# Python `random.randint(a, b)` calls, keyed per world (env = world id, episode = number of
+# reset_environment() calls so far, 0 for the create_* positions)
+SITE_T_CREATE = 7   # create_* spawn position      (WAB_Environment2.py:64-106)  tile (entity id, axis)
+SITE_T_RESET = 8    # reset spawn position         (WAB_Environment2_Single.py:43-48)  tile (entity id, axis)
+SITE_T_EAT = 9      # eat tie-break among bushes   (World.py:125)  turn, tile (ostrich id, 0)
+SITE_T_KILL = 10    # kill tie-break among ostriches (World.py:112)  turn, tile (wolf id, 0)
+
+
+def randint_keyed(ek: int, site: int, turn: int, x: int, y: int, a: int, b: int) -> int:
+    """Python's `random.randint(a, b)` (both ends included) under the keyed RNG:
+    a + floor(U * (b - a + 1) / 2^53), in exact integer arithmetic."""
+    U = int(draw_U(ek, site, turn, [x], [y], 0)[0])
+    return a + ((U * (b - a + 1)) >> 53)
 
 
 def mix64(z: int) -> int:

@@ -23,9 +23,10 @@ def build(quiet=True):
 
 
 def _stale():
-    srcs = [os.path.join(HERE, f) for f in ("wab_oracle.c", "wab_oracle.h", "Makefile")]
+    srcs = [os.path.join(HERE, f) for f in ("wab_oracle.c", "wab_oracle.h", "wab_torus_oracle.c", "Makefile")]
     srcs.append(os.path.join(os.path.dirname(HERE), "wab_gym_amd", "csrc", "wab_glyphs.h"))
     srcs.append(os.path.join(os.path.dirname(HERE), "include", "wab.h"))
+    srcs.append(os.path.join(os.path.dirname(HERE), "include", "wab_torus.h"))
     t = os.path.getmtime(LIB_PATH)
     return any(os.path.exists(s) and os.path.getmtime(s) > t for s in srcs)
 

@@ -13,12 +13,15 @@ from wab_gym_amd.options import WabConfig
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "wab.h")
+HEADERS = [HEADER, os.path.join(REPO, "include", "wab_torus.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(wab_[a-z_]+)\s*\(", src)))
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(wab2?_[a-z_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_header_declares_the_boundary():
@@ -105,3 +108,44 @@ def test_c_bush_thresholds_rejects_bad_arguments():
     assert L.wab_bush_thresholds(100.0, 256, None) == -1
     assert L.wab_bush_thresholds(float("nan"), 10, None) == -1
     assert L.wab_bush_thresholds(100.0, 10, None) == -1
+
+
+def test_torus_config_layout_matches_c(tmp_path):
+    """wab_torus.h's wab2_config and wab2_counters against their ctypes mirrors."""
+    from wab_gym_amd.torus_options import Wab2Config
+
+    fields = [f for f, _ in Wab2Config._fields_]
+    hdr = os.path.join(REPO, "include", "wab_torus.h")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % hdr, "int main(void){",
+             'printf("%zu\\n", sizeof(wab2_config));']
+    lines += ['printf("%%zu\\n", offsetof(wab2_config, %s));' % f for f in fields]
+    lines += ['printf("%zu\\n", sizeof(wab2_counters));', "return 0;}"]
+    prog = tmp_path / "layout2.c"
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "layout2"
+    subprocess.run(["gcc", "-o", str(exe), str(prog)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(Wab2Config)
+    for i, f in enumerate(fields):
+        assert int(out[1 + i]) == getattr(Wab2Config, f).offset, f
+    assert int(out[-1]) == ctypes.sizeof(_lib.Wab2Counters)
+
+
+def test_torus_record_size_and_validation_on_host():
+    """wab2_record_size is host-only: round_up(24 + 2N + NB, 16); invalid options -> -1."""
+    from wab_gym_amd.torus_options import make_config, record_size
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libwab_hip.so not built")
+    L = _lib.load()
+    assert L.wab2_abi_version() == _lib.ABI2_VERSION
+    for counts in ((1, 8, 16), (3, 4, 9), (2, 6, 10), (1, 3, 5), (8, 0, 24), (0, 0, 1)):
+        cfg, _ = make_config(32, 32, *counts)
+        assert L.wab2_record_size(ctypes.addressof(cfg)) == record_size(sum(counts), counts[2])
+    assert record_size(25, 16) == 96
+    cfg, _ = make_config(32, 32, 1, 8, 16)
+    cfg.num_ostriches = 9
+    assert L.wab2_record_size(ctypes.addressof(cfg)) == -1
+    assert b"ostriches" in L.wab2_last_error()
+    cfg.num_ostriches, cfg.width = 1, 128
+    assert L.wab2_record_size(ctypes.addressof(cfg)) == -1

@@ -19,7 +19,12 @@ EXPORTED = [
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
     "wab_debug_bush_values", "wab_step_features", "wab_discounted_returns_exact",
     "wab_bush_thresholds", "wab_rollout_features", "wab_render_envs",
+    # include/wab_torus.h: the Environment 2.0 torus world
+    "wab2_abi_version", "wab2_last_error", "wab2_record_size", "wab2_create", "wab2_destroy",
+    "wab2_batch", "wab2_reset", "wab2_step", "wab2_rollout", "wab2_get_state", "wab2_get_counters",
 ]
+
+ABI2_VERSION = 1
 
 ABI_VERSION = 4
 
@@ -84,13 +89,41 @@ def load():
     L.wab_batch.restype = I64
     L.wab_step_kernel.argtypes = [P]
     L.wab_step_kernel.restype = ctypes.c_char_p
+    L.wab2_abi_version.restype = ctypes.c_int
+    L.wab2_last_error.restype = ctypes.c_char_p
+    L.wab2_record_size.argtypes = [P]
+    L.wab2_create.argtypes = [P, I64, U64, I64, ctypes.c_int, ctypes.POINTER(P)]
+    L.wab2_destroy.argtypes = [P]
+    L.wab2_batch.argtypes = [P]
+    L.wab2_batch.restype = I64
+    L.wab2_reset.argtypes = [P, P, P]
+    L.wab2_step.argtypes = [P, P, P, P, P, P, P]
+    L.wab2_rollout.argtypes = [P, P, I32, P, P, P, P, P]
+    L.wab2_get_state.argtypes = [P] * 9
+    L.wab2_get_counters.argtypes = [P, P, P]
     for name in EXPORTED:
-        if name not in ("wab_abi_version", "wab_last_error", "wab_batch", "wab_step_kernel"):
+        if name not in ("wab_abi_version", "wab_last_error", "wab_batch", "wab_step_kernel",
+                        "wab2_abi_version", "wab2_last_error", "wab2_batch"):
             getattr(L, name).restype = ctypes.c_int
     if L.wab_abi_version() != ABI_VERSION:
         raise WabError("libwab_hip.so ABI %d != %d" % (L.wab_abi_version(), ABI_VERSION))
+    if L.wab2_abi_version() != ABI2_VERSION:
+        raise WabError("libwab_hip.so torus ABI %d != %d" % (L.wab2_abi_version(), ABI2_VERSION))
     _lib = L
     return L
+
+
+class Wab2Counters(ctypes.Structure):
+    _fields_ = [("turns", ctypes.c_uint64), ("resets", ctypes.c_uint64)]
+
+
+def check2(rc, what="wab2 call"):
+    """check() for the torus entry points (their own wab2_last_error)."""
+    if rc != 0:
+        msg = load().wab2_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError("%s: %s" % (what, msg))
+        raise WabError("%s failed (%d): %s" % (what, rc, msg))
 
 
 def check(rc, what="wab call"):

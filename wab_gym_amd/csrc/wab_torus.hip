@@ -1,0 +1,905 @@
+// wab_torus.hip — the batched Environment 2.0 torus world (include/wab_torus.h): kernels + C-ABI.
+//
+// Reference: `Environment 2.0/World.py` (get_observations :360-377, _get_visible_objects
+// :243-316, perform_entity_action :325-334, default_game_update :93-132, reset_world
+// :350-358), `WAB_Environment2.py` (create_* :61-110, reset_environment :113-118, take_action
+// :125-134), the entity classes (`Ostrich.py`, `Wolf.py`, `Bush.py`).  Checked bit for bit
+// against oracle/wab_torus_oracle.c and the golden vectors of the unmodified reference
+// (tests/test_gpu_torus.py).
+//
+// One workgroup (256 threads, 4 waves) owns 64 worlds for all T turns of a launch; their
+// state lives in LDS tables [entity][world] between turns (loaded by the first turn, stored
+// by the last).  A turn of the reference is N sequential take_action calls, but the only
+// cross-entity effects inside a turn are (a) positions: entity j's frame X/Y changes at its
+// own act only, so observer i sees entity j at its NEW position iff j < i; (b) kills: a
+// wolf's update hides an ostrich label for the observers after it; (c) eats: an ostrich's
+// update lowers one bush's food for the observers after it.  So a turn is:
+//   phase A  the sequential part, one lane per world: W0 moves the ostriches and resolves
+//            their eats, W1 moves the wolves and resolves their kills (and the autoreset
+//            decision), W2 moves the bushes (X = x mod W), W3 fetches the next turn's actions
+//            with scalar loads (no wait on its stores);
+//   phase B  every observation record, one lane per (world, observer) item, all four waves,
+//            from the LDS tables; records go through a per-wave LDS stage so each store
+//            instruction writes 1 KiB contiguous;
+//   phase C  the turn's end, one lane per (entity, world): positions, roles, status,
+//            Visible, food, autoreset draws.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wab_torus.h"
+#include "wab_device.h"
+
+namespace wab2 {
+
+using wab::draw_U;
+using wab::episode_key;
+using wab::lds_barrier;
+using wab::make_ts;
+using wab::xy_pack;
+
+enum : uint32_t { SITE_T_CREATE = 7, SITE_T_RESET = 8, SITE_T_EAT = 9, SITE_T_KILL = 10 };
+enum { T_OSTRICH = 0, T_WOLF = 1, T_BUSH = 2 };
+constexpr int kWorlds = 64;   // worlds per workgroup
+constexpr int kThreads = 256;
+constexpr int kNMax = WAB2_MAX_ENTITIES;
+constexpr int kOMax = WAB2_MAX_OSTRICHES;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ostrich state byte: status (bits 0-1), role (bit 2), Visible (bit 3)
+__device__ __forceinline__ int ost_status(uint32_t b) { return (int)(b & 3u); }
+__device__ __forceinline__ int ost_role(uint32_t b) { return (int)((b >> 2) & 1u); }
+__device__ __forceinline__ bool ost_visible(uint32_t b) { return (b >> 3) & 1u; }
+
+struct TParams {
+  // per-world state, SoA, world innermost ([entity][Bp])
+  int32_t* ox;          // [N][Bp] the entity object's own x (unbounded for movers)
+  int32_t* oy;          // [N][Bp]
+  uint16_t* df;         // [N][Bp] the frame's X | Y << 8
+  double* food;         // [NM][Bp] ostrich and wolf food
+  uint8_t* bfood;       // [NB][Bp] bush food
+  uint8_t* ost;         // [NO][Bp] ostrich state byte
+  int32_t* turn;        // [Bp] World._current_turn
+  uint32_t* episode;    // [Bp] reset_environment() calls
+  unsigned long long* counters;  // [2]: turns, resets
+  // I/O of a step / rollout launch
+  const int8_t* actions;  // [T][B][N]
+  uint8_t* obs;           // [T][B][N][R]
+  float* reward;          // [T][B][N]
+  uint8_t* done;          // [T][B][N]
+  uint8_t* world_reset;   // [T][B] or null
+  const uint8_t* mask;    // reset kernel: [B] or null
+  int64_t B, Bp, world_base;
+  uint64_t seed;
+  int32_t T, N, NO, NW, NB, NM, R, W, H;
+  int32_t rl, rg, rw;     // lookout, gatherer, wolf view radius
+  int32_t fpb, fg;        // food_per_bush, food_given_per_turn
+  double ofood0, wfood0, wff;
+  int32_t role0, max_turns, autoreset;
+  uint32_t magic_n;       // ceil(2^20 / N): q / N for q < 2048
+  int32_t act_scalar;     // actions may be read with scalar loads (4-byte aligned slices)
+};
+
+__device__ __forceinline__ int pymod(int a, int m) {
+  const int r = a % m;
+  return r < 0 ? r + m : r;
+}
+
+// random.randint(0, n - 1) under the keyed RNG: floor(U n / 2^53)
+__device__ __forceinline__ int keyed_below(uint64_t ek, uint32_t site, int32_t turn, int32_t x, int32_t y, uint32_t n) {
+  const uint64_t U = draw_U(xy_pack(x, y), make_ts(site, 0, turn), (uint32_t)ek, (uint32_t)(ek >> 32));
+  return (int)((U * (uint64_t)n) >> 53);
+}
+
+// the ostrich and wolf act tables (World.py:25-43, 61-73): 0 up (y+1), 1 right, 2 down, 3 left
+__device__ __forceinline__ int move_dx(int a) { return (a == 1) - (a == 3); }
+__device__ __forceinline__ int move_dy(int a) { return (a == 0) - (a == 2); }
+
+// LDS tables of the workgroup's 64 worlds (byte offsets from the dynamic LDS base)
+struct Lds {
+  double* food;      // [NM][64] turn start
+  int2* oxy;         // [NM][64] movers' own x, y (turn start)
+  uint8_t* stage;    // [4][32][R] record stage, per wave
+  uint8_t* act0;     // [64][N] raw actions (world-major, as in HBM) of even turns
+  uint8_t* act1;     // ... of odd turns
+  uint32_t* pos;     // [N][64] lo16: frame X|Y<<8 at turn start; hi16: after the entity's act
+  int32_t* turn;     // [64]
+  uint32_t* ep;      // [64]
+  uint32_t* ep_reset;  // [64] episode of this turn's reset draws, 0: no reset
+  uint16_t* bxy;     // [NB][64] bushes' own x | y << 8
+  uint16_t* ev;      // [NO][64] eat of ostrich k this turn: bush index | food after << 8 (0xFF: none)
+  uint8_t* gain;     // [NM][64] ostrich: berries eaten; wolf: 1 if it ate an ostrich
+  uint8_t* bf0;      // [NB][64] bush food at turn start
+  uint8_t* bf1;      // [NB][64] after the ostriches' eats
+  uint8_t* ost;      // [NO][64] ostrich state byte at turn start
+  uint8_t* hid;      // [NO][64] the wolf whose kill hid label k this turn (0xFF: none)
+  uint8_t* killed;   // [NO][64] status set to 2 this turn
+};
+
+__host__ __device__ inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+struct LdsLayout {
+  size_t food, oxy, stage, act0, act1, pos, turn, ep, ep_reset, bxy, ev, gain, bf0, bf1, ost, hid, killed, total;
+};
+
+__host__ __device__ inline LdsLayout lds_layout(int N, int NO, int NM, int NB, int R) {
+  LdsLayout L;
+  size_t o = 0;
+  L.food = o; o += align16((size_t)NM * kWorlds * 8);
+  L.oxy = o; o += align16((size_t)NM * kWorlds * 8);
+  L.stage = o; o += (size_t)4 * 32 * R;
+  L.act0 = o; o += align16((size_t)kWorlds * N);
+  L.act1 = o; o += align16((size_t)kWorlds * N);
+  L.pos = o; o += (size_t)N * kWorlds * 4;
+  L.turn = o; o += kWorlds * 4;
+  L.ep = o; o += kWorlds * 4;
+  L.ep_reset = o; o += kWorlds * 4;
+  L.bxy = o; o += align16((size_t)NB * kWorlds * 2);
+  L.ev = o; o += align16((size_t)NO * kWorlds * 2);
+  L.gain = o; o += align16((size_t)NM * kWorlds);
+  L.bf0 = o; o += align16((size_t)NB * kWorlds);
+  L.bf1 = o; o += align16((size_t)NB * kWorlds);
+  L.ost = o; o += align16((size_t)NO * kWorlds);
+  L.hid = o; o += align16((size_t)NO * kWorlds);
+  L.killed = o; o += align16((size_t)NO * kWorlds);
+  L.total = o;
+  return L;
+}
+
+__device__ __forceinline__ Lds lds_tables(uint8_t* base, const TParams& p) {
+  const LdsLayout L = lds_layout(p.N, p.NO, p.NM, p.NB, p.R);
+  Lds s;
+  s.food = reinterpret_cast<double*>(base + L.food);
+  s.oxy = reinterpret_cast<int2*>(base + L.oxy);
+  s.stage = base + L.stage;
+  s.act0 = base + L.act0;
+  s.act1 = base + L.act1;
+  s.pos = reinterpret_cast<uint32_t*>(base + L.pos);
+  s.turn = reinterpret_cast<int32_t*>(base + L.turn);
+  s.ep = reinterpret_cast<uint32_t*>(base + L.ep);
+  s.ep_reset = reinterpret_cast<uint32_t*>(base + L.ep_reset);
+  s.bxy = reinterpret_cast<uint16_t*>(base + L.bxy);
+  s.ev = reinterpret_cast<uint16_t*>(base + L.ev);
+  s.gain = base + L.gain;
+  s.bf0 = base + L.bf0;
+  s.bf1 = base + L.bf1;
+  s.ost = base + L.ost;
+  s.hid = base + L.hid;
+  s.killed = base + L.killed;
+  return s;
+}
+
+__device__ __forceinline__ uint64_t world_key(const TParams& p, int64_t g, uint32_t ep) {
+  return episode_key(p.seed, (uint64_t)(p.world_base + g), ep);
+}
+
+// A fresh copy of the kernel parameters, loaded from the kernel-argument segment behind an
+// opaque pointer (wab_device.h kernel_params): each phase loads the fields it uses, instead of
+// the whole block being held in (and spilled from) scalar registers across the turn loop.
+__device__ __forceinline__ TParams kparams(const TParams& p0) {
+#if __HIP_DEVICE_COMPILE__
+  typedef const TParams __attribute__((address_space(4))) KP;
+  KP* pk = (KP*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  return *pk;
+#else
+  return p0;
+#endif
+}
+
+// actions of turn t for the workgroup's worlds into act (raw [64][N] bytes).  Scalar loads
+// (counted in lgkmcnt, so nothing waits on the wave's stores) when the slice is 4-byte aligned
+// and the workgroup is full; per-byte vector loads otherwise.
+__device__ __forceinline__ void fetch_actions_wave(const TParams& p, int t, int64_t wg0, int nvalid, uint8_t* act,
+                                                   int lane) {
+  const int nbytes = kWorlds * p.N;
+  const int8_t* src = p.actions + (int64_t)t * p.B * p.N + wg0 * p.N;
+  if (p.act_scalar && nvalid == kWorlds) {
+    typedef const uint32_t __attribute__((address_space(4))) CU32;
+    CU32* c = (CU32*)reinterpret_cast<uintptr_t>(src);
+    asm volatile("" : "+s"(c));
+    for (int ch = 0; ch < nbytes / 64; ++ch) {  // 64-byte chunks (64 * N is a multiple of 64)
+      uint32_t v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = c[ch * 16 + k];
+      uint32_t d = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) d = lane == k ? v[k] : d;
+      if (lane < 16) reinterpret_cast<uint32_t*>(act)[ch * 16 + lane] = d;
+    }
+  } else {
+    for (int q = lane; q < nbytes; q += 64)
+      act[q] = q < nvalid * p.N ? (uint8_t)src[q] : (uint8_t)0;
+  }
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) wab_torus_kernel(TParams p0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int64_t wg0 = (int64_t)blockIdx.x * kWorlds;
+  const int nvalid = (int)min((int64_t)kWorlds, p0.B - wg0);
+  const int T = p0.T;
+// every phase works from its own copy of the parameters and LDS table pointers (kparams)
+#define WAB2_PHASE_PARAMS                                                                   \
+  const TParams p = kparams(p0);                                                          \
+  const Lds s = lds_tables(smem, p);                                                      \
+  const int N = p.N, NO = p.NO, NM = p.NM, NB = p.NB, R = p.R, W = p.W, H = p.H;          \
+  const int nent = N * kWorlds;                                                           \
+  (void)NO; (void)NM; (void)NB; (void)R; (void)W; (void)H; (void)nent
+
+  // ---- prologue: state -> LDS tables, one lane per (entity, world); turn 0's actions
+  {
+  WAB2_PHASE_PARAMS;
+  for (int q = tid; q < nent; q += kThreads) {
+    const int e = q >> 6, w = q & 63;
+    const int64_t a = (int64_t)e * p.Bp + wg0 + w;
+    s.pos[e * kWorlds + w] = p.df[a];
+    if (e < NM) {
+      s.oxy[e * kWorlds + w] = make_int2(p.ox[a], p.oy[a]);
+      s.food[e * kWorlds + w] = p.food[(int64_t)e * p.Bp + wg0 + w];
+    } else {
+      const int b = e - NM;
+      s.bxy[b * kWorlds + w] = (uint16_t)((p.ox[a] & 0xFF) | ((p.oy[a] & 0xFF) << 8));
+      s.bf0[b * kWorlds + w] = p.bfood[(int64_t)b * p.Bp + wg0 + w];
+    }
+    if (e < NO) s.ost[e * kWorlds + w] = p.ost[(int64_t)e * p.Bp + wg0 + w];
+    if (e == 0) {
+      s.turn[w] = p.turn[wg0 + w];
+      s.ep[w] = p.episode[wg0 + w];
+    }
+  }
+  {
+    const int8_t* src = p.actions + wg0 * N;
+    for (int q = tid; q < nent; q += kThreads) s.act0[q] = q < nvalid * N ? (uint8_t)src[q] : (uint8_t)0;
+  }
+  }
+  __syncthreads();
+
+  int64_t resets = 0;
+  for (int t = 0; t < T; ++t) {
+    // ================= phase A: the sequential part of the turn, one lane per world
+    if (wave == 0) {
+      WAB2_PHASE_PARAMS;
+      const uint8_t* A = (t & 1) ? s.act1 : s.act0;
+      // ostriches in id order: act (World.py:25-43), X = x mod W (:331-332), eat (:118-132)
+      const int w = lane;
+      for (int b = 0; b < NB; ++b) s.bf1[b * kWorlds + w] = s.bf0[b * kWorlds + w];
+      const uint64_t ek = world_key(p, wg0 + w, s.ep[w]);
+      const int32_t turn = s.turn[w];
+      for (int k = 0; k < NO; ++k) {
+        const int a = (int)(int8_t)A[w * N + k];
+        const int2 xy = s.oxy[k * kWorlds + w];
+        const uint32_t np = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
+        reinterpret_cast<uint16_t*>(&s.pos[k * kWorlds + w])[1] = (uint16_t)np;
+        // the visible bushes on the tile, in frame (id) order: every bush is visible (the
+        // Visible update of World.py:131 writes a copy), at its turn-start frame position
+        int n = 0;
+        for (int b = 0; b < NB; ++b) n += (s.pos[(NM + b) * kWorlds + w] & 0xFFFFu) == np;
+        uint32_t ev = 0xFFu, gain = 0;
+        if (n > 0) {
+          int j = keyed_below(ek, SITE_T_EAT, turn, k, 0, (uint32_t)n);
+          int pick = 0;
+          for (int b = 0; b < NB; ++b)
+            if ((s.pos[(NM + b) * kWorlds + w] & 0xFFFFu) == np) {
+              if (j == 0) pick = b;
+              --j;
+            }
+          // Bush.take_food (Bush.py:31-39)
+          int f = s.bf1[pick * kWorlds + w];
+          const int amt = f >= p.fg ? p.fg : f;
+          f = f >= p.fg ? f - p.fg : 0;
+          s.bf1[pick * kWorlds + w] = (uint8_t)f;
+          ev = (uint32_t)pick | ((uint32_t)f << 8);
+          gain = (uint32_t)amt;
+        }
+        s.ev[k * kWorlds + w] = (uint16_t)ev;
+        s.gain[k * kWorlds + w] = (uint8_t)gain;
+      }
+    } else if (wave == 1) {
+      WAB2_PHASE_PARAMS;
+      const uint8_t* A = (t & 1) ? s.act1 : s.act0;
+      // wolves in id order: act (World.py:61-73), X = x mod W, kill (:107-116)
+      const int w = lane;
+      const uint64_t ek = world_key(p, wg0 + w, s.ep[w]);
+      const int32_t turn = s.turn[w];
+      uint32_t opos[kOMax];  // the ostriches' frame X|Y after their acts (they act first)
+      uint32_t vis = 0, dead = 0, kills = 0, hid_by[kOMax];
+#pragma unroll
+      for (int k = 0; k < kOMax; ++k) {
+        opos[k] = 0xFFFFFFFFu;
+        hid_by[k] = 0xFFu;
+        if (k < NO) {
+          const int a = (int)(int8_t)A[w * N + k];
+          const int2 xy = s.oxy[k * kWorlds + w];
+          opos[k] = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
+          const uint32_t ob = s.ost[k * kWorlds + w];
+          vis |= (uint32_t)ost_visible(ob) << k;
+          dead |= (uint32_t)(ost_status(ob) != 0) << k;
+        }
+      }
+      for (int m = NO; m < NM; ++m) {
+        const int a = (int)(int8_t)A[w * N + m];
+        const int2 xy = s.oxy[m * kWorlds + w];
+        const uint32_t np = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
+        reinterpret_cast<uint16_t*>(&s.pos[m * kWorlds + w])[1] = (uint16_t)np;
+        uint32_t cand = 0;
+#pragma unroll
+        for (int k = 0; k < kOMax; ++k) cand |= (uint32_t)((vis >> k & 1u) && opos[k] == np) << k;
+        uint32_t gain = 0;
+        if (cand) {
+          const int n = __builtin_popcount(cand);
+          const int j = keyed_below(ek, SITE_T_KILL, turn, m, 0, (uint32_t)n);
+          uint32_t c = cand;
+          for (int r = 0; r < j; ++r) c &= c - 1;
+          kills |= c & (0u - c);  // the j-th visible ostrich of the tile: status 2 (:114)
+          gain = 1;
+          // `loc[j, "Visible"] = False` (:115): the frame LABEL j, an ostrich id since the
+          // ostriches were created first
+#pragma unroll
+          for (int k = 0; k < kOMax; ++k)
+            if (k == j && (vis >> k & 1u)) {
+              vis &= ~(1u << k);
+              hid_by[k] = (uint32_t)m;
+            }
+        }
+        s.gain[m * kWorlds + w] = (uint8_t)gain;
+      }
+#pragma unroll
+      for (int k = 0; k < kOMax; ++k)
+        if (k < NO) {
+          s.hid[k * kWorlds + w] = (uint8_t)hid_by[k];
+          s.killed[k * kWorlds + w] = (uint8_t)(kills >> k & 1u);
+        }
+      dead |= kills;
+      // the batched surface's autoreset: every ostrich done, or max_turns reached
+      const bool all_dead = NO > 0 && dead == (NO >= 32 ? 0xFFFFFFFFu : (1u << NO) - 1u);
+      const bool rs = p.autoreset && (all_dead || (p.max_turns > 0 && turn + 1 >= p.max_turns));
+      s.ep_reset[w] = rs ? s.ep[w] + 1u : 0u;
+      const bool valid = w < nvalid;
+      if (p.world_reset && valid) p.world_reset[(int64_t)t * p.B + wg0 + w] = (uint8_t)rs;
+      resets += (rs && valid) ? 1 : 0;
+    } else if (wave == 2) {
+      WAB2_PHASE_PARAMS;
+      // bushes act on nothing (World.py:9-10); their frame X/Y become x mod W, y mod H
+      const int w = lane;
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t bxy = s.bxy[b * kWorlds + w];
+        const uint32_t np = (uint32_t)pymod((int)(bxy & 0xFFu), W) | ((uint32_t)pymod((int)(bxy >> 8), H) << 8);
+        reinterpret_cast<uint16_t*>(&s.pos[(NM + b) * kWorlds + w])[1] = (uint16_t)np;
+      }
+    } else if (t + 1 < T) {
+      WAB2_PHASE_PARAMS;
+      fetch_actions_wave(p, t + 1, wg0, nvalid, (t & 1) ? s.act0 : s.act1, lane);
+    }
+    __syncthreads();
+
+    // ================= phase B: observation records, reward, done.  Rounds of 32 (world,
+    // observer) items per wave; lanes l and l + 32 share item l: each computes half of the
+    // observer's view (delta dwords k = 2kk + half, i.e. entities 4kk + 2 half + {0, 1}), so a
+    // round's 32 records fit the wave's LDS stage and every lane is busy
+    {
+      WAB2_PHASE_PARAMS;
+      const int nitems = nvalid * N;
+      uint8_t* stage = s.stage + wave * 32 * R;
+      const int64_t item0 = wg0 * N;  // first item of the workgroup in [B][N]
+      uint8_t* obs_t = p.obs + (int64_t)t * p.B * N * R;
+      const int hf = lane >> 5;
+      const int nd = (2 * N + 3) >> 2;  // delta dwords
+      const int bb = 24 + 2 * N;        // first bush-food byte
+      for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
+        const int q = rnd * 32 + (lane & 31);
+        const bool on = q < nitems;
+        const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
+        const int w = (int)(((uint32_t)qc * p.magic_n) >> 20);
+        const int i = qc - w * N;
+        const int type = i < NO ? T_OSTRICH : i < NM ? T_WOLF : T_BUSH;
+        const uint32_t pi = s.pos[i * kWorlds + w];
+        const int ex = (int)(pi & 0xFFu), ey = (int)((pi >> 8) & 0xFFu);
+        const uint32_t ob = type == T_OSTRICH ? s.ost[i * kWorlds + w] : 0u;
+        const int role = ost_role(ob), status = ost_status(ob);
+        // World.get_observations (:365-374)
+        const int r = type == T_OSTRICH ? (role == 1 ? p.rg : p.rl) : type == T_WOLF ? p.rw : 0;
+        const int rc = min(r, 255);
+        const int r2 = rc * rc;  // (dx^2 + dy^2) ** 0.5 <= r  <=>  dx^2 + dy^2 <= r^2 (integers)
+        // the wrap of World.py:255-291 as thresholds on dx: the `if` side replaces dx by
+        // dx - W when X >= W - (r - x) and |dx - W| < |dx|; the `elif` side by dx + W
+        const int lox = ex < r ? W - r : 0x7FFF, hix = (ex >= r && W < ex + r) ? r - W : -0x7FFF;
+        const int loy = ey < r ? H - r : 0x7FFF, hiy = (ey >= r && H < ey + r) ? r - H : -0x7FFF;
+        // ostriches still Visible when i observes: visible at the turn start and not hidden
+        // by a wolf that acted before i
+        uint32_t alive = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < kOMax; ++k)
+          if (k < NO) {
+            const uint32_t okb = s.ost[k * kWorlds + w];
+            const int h = s.hid[k * kWorlds + w];
+            if (!ost_visible(okb) || h < i) alive &= ~(1u << k);
+          }
+        uint32_t vis = 0, d[NMAX / 4];
+#pragma unroll
+        for (int kk = 0; kk < NMAX / 4; ++kk) {
+          d[kk] = 0;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int j = 4 * kk + 2 * hf + u;
+            if (j < N) {
+              const uint32_t pj = s.pos[j * kWorlds + w];
+              const uint32_t xy = j < i ? pj >> 16 : pj & 0xFFFFu;
+              int dx = (int)(xy & 0xFFu) - ex, dy = (int)(xy >> 8) - ey;
+              dx = (dx >= lox && 2 * dx > W) ? dx - W : dx;
+              dx = (dx <= hix && 2 * dx < -W) ? dx + W : dx;
+              dy = (dy >= loy && 2 * dy > H) ? dy - H : dy;
+              dy = (dy <= hiy && 2 * dy < -H) ? dy + H : dy;
+              const bool ok = dx * dx + dy * dy <= r2 && (alive >> j & 1u);
+              vis |= (uint32_t)ok << j;
+              const uint32_t pair = ((uint32_t)dx & 0xFFu) | (((uint32_t)dy & 0xFFu) << 8);
+              d[kk] |= ok ? pair << (16 * u) : 0u;
+            }
+          }
+        }
+        vis |= __shfl_xor(vis, 32);
+        // internal obs (World.py:17-18, 50-51, 80-81)
+        double food;
+        int x, y;
+        if (type == T_BUSH) {
+          const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
+          x = (int)(bxy & 0xFFu);
+          y = (int)(bxy >> 8);
+          food = (double)s.bf1[(i - NM) * kWorlds + w];  // the bushes act after every ostrich
+        } else {
+          const int2 xy = s.oxy[i * kWorlds + w];
+          x = xy.x;
+          y = xy.y;
+          food = s.food[i * kWorlds + w];
+        }
+        const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
+        if (on && hf == 0) {
+          // reward / done after the entity's own update (compute_reward, is_entity_done)
+          float rew;
+          uint8_t dn;
+          if (type == T_OSTRICH) {
+            rew = status == 0 ? 1.0f : 0.0f;
+            dn = status != 0;
+          } else if (type == T_WOLF) {
+            const double fa = s.gain[i * kWorlds + w] ? food + p.wff : food;
+            rew = fa > 10.0 ? 1.0f : 0.0f;
+            dn = 0;
+          } else {
+            rew = 0.0f;
+            dn = 1;
+          }
+          p.reward[(int64_t)t * p.B * N + item0 + q] = rew;
+          p.done[(int64_t)t * p.B * N + item0 + q] = dn;
+        }
+        uint8_t* rec = stage + (lane & 31) * R;
+        if (hf == 0) {
+          const uint64_t fb = (uint64_t)__double_as_longlong(food);
+          *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
+          *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
+        } else {
+          for (int z = 24 + 4 * nd; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
+        }
+#pragma unroll
+        for (int kk = 0; kk < NMAX / 4; ++kk)
+          if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+        // Additional_Data [food] of the visible bushes as the observer sees them: after the
+        // eats of the ostriches that acted before it
+        for (int b = hf; b < NB; b += 2) {
+          uint32_t f = 0;
+          if (vis >> (NM + b) & 1u) {
+            if (type == T_OSTRICH) {
+              f = s.bf0[b * kWorlds + w];
+              for (int k = 0; k < NO; ++k)
+                if (k < i) {
+                  const uint32_t e = s.ev[k * kWorlds + w];
+                  if ((e & 0xFFu) == (uint32_t)b) f = e >> 8;
+                }
+            } else {
+              f = s.bf1[b * kWorlds + w];
+            }
+          }
+          rec[bb + b] = (uint8_t)f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the round's records are contiguous in HBM: 16 bytes per lane, 1 KiB per instruction
+        const int q0 = rnd * 32;
+        const int cnt = min(32, nitems - q0);
+        const int chunks = cnt * R / 16;
+        uint8_t* dst = obs_t + (item0 + q0) * (int64_t)R;
+        for (int c = lane; c < chunks; c += 64) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16 * c);
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + 16 * c));
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();
+
+    // ================= phase C: the turn's end, one lane per (entity, world)
+    {
+    WAB2_PHASE_PARAMS;
+    const uint8_t* A = (t & 1) ? s.act1 : s.act0;
+    for (int q = tid; q < nent; q += kThreads) {
+      const int e = q >> 6, w = q & 63;
+      const uint32_t epr = s.ep_reset[w];
+      uint32_t pe = s.pos[e * kWorlds + w];
+      s.pos[e * kWorlds + w] = pe >> 16;  // the frame X/Y after the act (a reset leaves it)
+      const int a = (int)(int8_t)A[w * N + e];
+      int nx = 0, ny = 0;
+      if (epr) {  // reset_environment: randint(0, W), randint(0, H) (WAB_Environment2_Single.py:45-46)
+        const uint64_t ek = world_key(p, wg0 + w, epr);
+        nx = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)W + 1u);
+        ny = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)H + 1u);
+      }
+      if (e < NM) {
+        int2 xy = s.oxy[e * kWorlds + w];
+        xy.x += move_dx(a);
+        xy.y += move_dy(a);
+        double f = s.food[e * kWorlds + w];
+        const uint32_t g = s.gain[e * kWorlds + w];
+        if (e < NO) {
+          f += (double)g;
+          uint32_t ob = s.ost[e * kWorlds + w];
+          if (a == 4) ob &= ~4u;
+          if (a == 5) ob |= 4u;
+          if (s.killed[e * kWorlds + w]) ob = (ob & ~3u) | 2u;
+          if (s.hid[e * kWorlds + w] != 0xFFu) ob &= ~8u;
+          if (epr) ob = ((uint32_t)p.role0 << 2) | 8u;
+          s.ost[e * kWorlds + w] = (uint8_t)ob;
+          if (epr) f = p.ofood0;
+        } else {
+          if (g) f += p.wff;
+          if (epr) f = p.wfood0;
+        }
+        if (epr) xy = make_int2(nx, ny);
+        s.oxy[e * kWorlds + w] = xy;
+        s.food[e * kWorlds + w] = f;
+      } else {
+        const int b = e - NM;
+        s.bf0[b * kWorlds + w] = epr ? (uint8_t)p.fpb : s.bf1[b * kWorlds + w];
+        if (epr) s.bxy[b * kWorlds + w] = (uint16_t)(nx | (ny << 8));
+      }
+      if (e == 0) {
+        s.turn[w] = epr ? 0 : s.turn[w] + 1;
+        if (epr) s.ep[w] = epr;
+      }
+    }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: LDS tables -> state
+  {
+  WAB2_PHASE_PARAMS;
+  for (int q = tid; q < nent; q += kThreads) {
+    const int e = q >> 6, w = q & 63;
+    const int64_t a = (int64_t)e * p.Bp + wg0 + w;
+    p.df[a] = (uint16_t)s.pos[e * kWorlds + w];
+    if (e < NM) {
+      const int2 xy = s.oxy[e * kWorlds + w];
+      p.ox[a] = xy.x;
+      p.oy[a] = xy.y;
+      p.food[(int64_t)e * p.Bp + wg0 + w] = s.food[e * kWorlds + w];
+    } else {
+      const int b = e - NM;
+      const uint32_t bxy = s.bxy[b * kWorlds + w];
+      p.ox[a] = (int32_t)(bxy & 0xFFu);
+      p.oy[a] = (int32_t)(bxy >> 8);
+      p.bfood[(int64_t)b * p.Bp + wg0 + w] = s.bf0[b * kWorlds + w];
+    }
+    if (e < NO) p.ost[(int64_t)e * p.Bp + wg0 + w] = s.ost[e * kWorlds + w];
+    if (e == 0) {
+      p.turn[wg0 + w] = s.turn[w];
+      p.episode[wg0 + w] = s.ep[w];
+    }
+  }
+  }
+  if (wave == 1) {  // resets of this workgroup (W1 decided them), one atomic per wave
+    unsigned long long tot = (unsigned long long)resets;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    if (lane == 0 && tot) atomicAdd(&p0.counters[1], tot);
+  }
+  if (blockIdx.x == 0 && tid == 0) atomicAdd(&p0.counters[0], (unsigned long long)p0.B * (unsigned long long)T);
+#undef WAB2_PHASE_PARAMS
+}
+
+// create_ostriches / create_wolves / create_bushes with random positions: randint(0, W - 1),
+// randint(0, H - 1) per entity (WAB_Environment2.py:64-106), episode 0; one lane per world
+__global__ void wab_torus_create_kernel(TParams p) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= p.Bp) return;
+  const uint64_t ek = world_key(p, g, 0);
+  for (int e = 0; e < p.N; ++e) {
+    const int x = keyed_below(ek, SITE_T_CREATE, 0, e, 0, (uint32_t)p.W);
+    const int y = keyed_below(ek, SITE_T_CREATE, 0, e, 1, (uint32_t)p.H);
+    const int64_t a = (int64_t)e * p.Bp + g;
+    p.ox[a] = x;
+    p.oy[a] = y;
+    p.df[a] = (uint16_t)(x | (y << 8));
+    if (e < p.NM) p.food[a] = e < p.NO ? p.ofood0 : p.wfood0;
+    else p.bfood[(int64_t)(e - p.NM) * p.Bp + g] = (uint8_t)p.fpb;
+    if (e < p.NO) p.ost[(int64_t)e * p.Bp + g] = (uint8_t)((p.role0 << 2) | 8);
+  }
+  p.turn[g] = 0;
+  p.episode[g] = 0;
+}
+
+// reset_environment (WAB_Environment2.py:113-118) of the masked worlds; one lane per world
+__global__ void wab_torus_reset_kernel(TParams p) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= p.B || (p.mask && !p.mask[g])) return;
+  const uint32_t ep = p.episode[g] + 1u;
+  const uint64_t ek = world_key(p, g, ep);
+  for (int e = 0; e < p.N; ++e) {
+    const int x = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)p.W + 1u);
+    const int y = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)p.H + 1u);
+    const int64_t a = (int64_t)e * p.Bp + g;
+    p.ox[a] = x;
+    p.oy[a] = y;
+    if (e < p.NM) p.food[a] = e < p.NO ? p.ofood0 : p.wfood0;
+    else p.bfood[(int64_t)(e - p.NM) * p.Bp + g] = (uint8_t)p.fpb;
+    if (e < p.NO) p.ost[(int64_t)e * p.Bp + g] = (uint8_t)((p.role0 << 2) | 8);
+  }
+  p.turn[g] = 0;
+  p.episode[g] = ep;
+  atomicAdd(&p.counters[1], 1ull);
+}
+
+}  // namespace wab2
+
+using wab2::TParams;
+
+struct wab2_handle {
+  TParams p;
+  int device = 0;
+  int n_blocks = 0;
+  size_t lds = 0;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+thread_local std::string g_err2;
+
+int fail(int code, const std::string& msg) {
+  g_err2 = msg;
+  return code;
+}
+
+#define HIP_TRY2(expr)                                                                \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(WAB2_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard2 {
+  int prev = -1;
+  explicit DeviceGuard2(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard2() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int record_size(const wab2_config* c) {
+  const int N = c->num_ostriches + c->num_wolves + c->num_bushes;
+  return (24 + 2 * N + c->num_bushes + 15) / 16 * 16;
+}
+
+std::string validate(const wab2_config* c) {
+  if (!c) return "config is NULL";
+  if (c->width < 1 || c->width > WAB2_MAX_SIDE || c->height < 1 || c->height > WAB2_MAX_SIDE)
+    return "width and height must be in [1, 127]";
+  if (c->num_ostriches < 0 || c->num_wolves < 0 || c->num_bushes < 0) return "negative entity count";
+  if (c->num_ostriches > WAB2_MAX_OSTRICHES) return "at most 8 ostriches";
+  const int N = c->num_ostriches + c->num_wolves + c->num_bushes;
+  if (N < 1 || N > WAB2_MAX_ENTITIES) return "1 to 32 entities in all";
+  if (c->starting_role != 0 && c->starting_role != 1) return "starting_role must be 0 or 1";
+  if (c->food_per_bush < 0 || c->food_per_bush > 255 || c->food_given_per_turn < 0 || c->food_given_per_turn > 255)
+    return "food_per_bush and food_given_per_turn must be in [0, 255]";
+  if (c->lookout_view_radius < 0 || c->gatherer_view_radius < 0 || c->wolf_view_radius < 0)
+    return "view radii must be >= 0";
+  if (c->max_turns < 0) return "max_turns must be >= 0";
+  return "";
+}
+
+}  // namespace
+
+extern "C" {
+
+int wab2_abi_version(void) { return WAB2_ABI_VERSION; }
+const char* wab2_last_error(void) { return g_err2.c_str(); }
+int wab2_record_size(const wab2_config* cfg) {
+  const std::string v = validate(cfg);
+  if (!v.empty()) return fail(WAB2_E_INVALID, v);
+  return record_size(cfg);
+}
+
+int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t world_id_base, int device,
+                wab2_handle** out) {
+  if (!out) return fail(WAB2_E_INVALID, "out is NULL");
+  *out = nullptr;
+  const std::string v = validate(cfg);
+  if (!v.empty()) return fail(WAB2_E_INVALID, v);
+  if (batch < 1) return fail(WAB2_E_INVALID, "batch must be >= 1");
+  DeviceGuard2 dg(device);
+  wab2_handle* h = new wab2_handle();
+  h->device = device;
+  TParams& p = h->p;
+  p.N = cfg->num_ostriches + cfg->num_wolves + cfg->num_bushes;
+  p.NO = cfg->num_ostriches;
+  p.NW = cfg->num_wolves;
+  p.NB = cfg->num_bushes;
+  p.NM = p.NO + p.NW;
+  p.R = record_size(cfg);
+  p.W = cfg->width;
+  p.H = cfg->height;
+  p.rl = cfg->lookout_view_radius;
+  p.rg = cfg->gatherer_view_radius;
+  p.rw = cfg->wolf_view_radius;
+  p.fpb = cfg->food_per_bush;
+  p.fg = cfg->food_given_per_turn;
+  p.ofood0 = cfg->ostrich_starting_food;
+  p.wfood0 = cfg->wolf_starting_food;
+  p.wff = cfg->wolf_food_for_eating_ostrich;
+  p.role0 = cfg->starting_role;
+  p.max_turns = cfg->max_turns;
+  p.autoreset = cfg->autoreset ? 1 : 0;
+  p.magic_n = (uint32_t)(((1u << 20) + (uint32_t)p.N - 1u) / (uint32_t)p.N);
+  p.B = batch;
+  h->n_blocks = (int)((batch + wab2::kWorlds - 1) / wab2::kWorlds);
+  p.Bp = (int64_t)h->n_blocks * wab2::kWorlds;
+  p.seed = seed;
+  p.world_base = world_id_base;
+  const wab2::LdsLayout L = wab2::lds_layout(p.N, p.NO, p.NM, p.NB, p.R);
+  h->lds = L.total;
+  auto alloc = [&](void** ptr, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(ptr, bytes < 16 ? 16 : bytes);
+    if (e == hipSuccess) {
+      h->allocs.push_back(*ptr);
+      e = hipMemset(*ptr, 0, bytes < 16 ? 16 : bytes);
+    }
+    return e;
+  };
+  const size_t NBp = (size_t)p.Bp;
+  hipError_t e = hipSuccess;
+  void* q = nullptr;
+  if (e == hipSuccess) { e = alloc(&q, NBp * p.N * 4); p.ox = (int32_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * p.N * 4); p.oy = (int32_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * p.N * 2); p.df = (uint16_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * (p.NM ? p.NM : 1) * 8); p.food = (double*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * (p.NB ? p.NB : 1)); p.bfood = (uint8_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * (p.NO ? p.NO : 1)); p.ost = (uint8_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * 4); p.turn = (int32_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, NBp * 4); p.episode = (uint32_t*)q; }
+  if (e == hipSuccess) { e = alloc(&q, 2 * sizeof(unsigned long long)); p.counters = (unsigned long long*)q; }
+  if (e == hipSuccess && h->lds > 64 * 1024)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wab2::wab_torus_kernel<wab2::kNMax>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(wab2::wab_torus_create_kernel, dim3((unsigned)((p.Bp + 255) / 256)), dim3(256), 0, 0, p);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    for (void* a : h->allocs) (void)hipFree(a);
+    delete h;
+    return fail(e == hipErrorOutOfMemory ? WAB2_E_NOMEM : WAB2_E_HIP, std::string("wab2_create: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return WAB2_OK;
+}
+
+int wab2_destroy(wab2_handle* h) {
+  if (!h) return WAB2_OK;
+  DeviceGuard2 dg(h->device);
+  (void)hipDeviceSynchronize();
+  for (void* a : h->allocs) (void)hipFree(a);
+  delete h;
+  return WAB2_OK;
+}
+
+int64_t wab2_batch(const wab2_handle* h) { return h ? h->p.B : 0; }
+
+int wab2_reset(wab2_handle* h, const uint8_t* mask, void* stream) {
+  if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
+  DeviceGuard2 dg(h->device);
+  TParams p = h->p;
+  p.mask = mask;
+  hipLaunchKernelGGL(wab2::wab_torus_reset_kernel, dim3((unsigned)((p.B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, p);
+  HIP_TRY2(hipGetLastError());
+  return WAB2_OK;
+}
+
+int wab2_rollout(wab2_handle* h, const int8_t* actions, int32_t T, uint8_t* obs, float* reward, uint8_t* done,
+                 uint8_t* world_reset, void* stream) {
+  if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
+  if (T < 1) return fail(WAB2_E_INVALID, "T must be >= 1");
+  if (!actions || !obs || !reward || !done) return fail(WAB2_E_INVALID, "actions, obs, reward and done are required");
+  if (reinterpret_cast<uintptr_t>(obs) & 15u) return fail(WAB2_E_INVALID, "obs must be 16-byte aligned");
+  DeviceGuard2 dg(h->device);
+  TParams p = h->p;
+  p.T = T;
+  p.actions = actions;
+  p.obs = obs;
+  p.reward = reward;
+  p.done = done;
+  p.world_reset = world_reset;
+  p.act_scalar = ((reinterpret_cast<uintptr_t>(actions) & 3u) == 0u && (p.B * p.N) % 4 == 0) ? 1 : 0;
+  hipLaunchKernelGGL(wab2::wab_torus_kernel<wab2::kNMax>, dim3((unsigned)h->n_blocks), dim3(wab2::kThreads), h->lds,
+                     (hipStream_t)stream, p);
+  HIP_TRY2(hipGetLastError());
+  return WAB2_OK;
+}
+
+int wab2_step(wab2_handle* h, const int8_t* actions, uint8_t* obs, float* reward, uint8_t* done,
+              uint8_t* world_reset, void* stream) {
+  return wab2_rollout(h, actions, 1, obs, reward, done, world_reset, stream);
+}
+
+int wab2_get_state(wab2_handle* h, int32_t* df_xy, int32_t* obj_xy, double* food, uint8_t* visible, uint8_t* status,
+                   int32_t* turn, uint32_t* episode, void* stream) {
+  if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
+  DeviceGuard2 dg(h->device);
+  const TParams& p = h->p;
+  HIP_TRY2(hipStreamSynchronize((hipStream_t)stream));
+  const size_t Bp = (size_t)p.Bp, B = (size_t)p.B, N = (size_t)p.N;
+  std::vector<int32_t> ox(Bp * N), oy(Bp * N), tn(Bp);
+  std::vector<uint16_t> df(Bp * N);
+  std::vector<double> fd(Bp * (p.NM ? p.NM : 1));
+  std::vector<uint8_t> bf(Bp * (p.NB ? p.NB : 1)), os(Bp * (p.NO ? p.NO : 1));
+  std::vector<uint32_t> ep(Bp);
+  HIP_TRY2(hipMemcpy(ox.data(), p.ox, ox.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(oy.data(), p.oy, oy.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(df.data(), p.df, df.size() * 2, hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(fd.data(), p.food, fd.size() * 8, hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(bf.data(), p.bfood, bf.size(), hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(os.data(), p.ost, os.size(), hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(tn.data(), p.turn, tn.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY2(hipMemcpy(ep.data(), p.episode, ep.size() * 4, hipMemcpyDeviceToHost));
+  for (size_t b = 0; b < B; ++b) {
+    for (size_t e = 0; e < N; ++e) {
+      const size_t a = e * Bp + b, q = b * N + e;
+      if (df_xy) {
+        df_xy[2 * q] = df[a] & 0xFF;
+        df_xy[2 * q + 1] = df[a] >> 8;
+      }
+      if (obj_xy) {
+        obj_xy[2 * q] = ox[a];
+        obj_xy[2 * q + 1] = oy[a];
+      }
+      if (food) food[q] = (int)e < p.NM ? fd[a] : (double)bf[(e - p.NM) * Bp + b];
+      if (visible) visible[q] = (int)e < p.NO ? (uint8_t)((os[a] >> 3) & 1) : (uint8_t)1;
+      if (status && (int)e < p.NO) status[b * p.NO + e] = (uint8_t)(os[a] & 3);
+    }
+    if (turn) turn[b] = tn[b];
+    if (episode) episode[b] = ep[b];
+  }
+  return WAB2_OK;
+}
+
+int wab2_get_counters(wab2_handle* h, wab2_counters* out, void* stream) {
+  if (!h || !out) return fail(WAB2_E_INVALID, "handle or out is NULL");
+  DeviceGuard2 dg(h->device);
+  HIP_TRY2(hipStreamSynchronize((hipStream_t)stream));
+  unsigned long long c[2];
+  HIP_TRY2(hipMemcpy(c, h->p.counters, sizeof(c), hipMemcpyDeviceToHost));
+  out->turns = c[0];
+  out->resets = c[1];
+  return WAB2_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,209 @@
+"""BatchedWABEnvironment2 — `Environment 2.0/WAB_Environment2.py` with a leading batch dimension.
+
+The reference's multi-entity torus world: `WAB_Environment2(W, H, options)`,
+`create_ostriches(n)`, `create_wolves(n)`, `create_bushes(n)`, `reset_environment()`, and per
+entity `get_obs(i)` / `take_action(i, a) -> (reward, done)` (WAB_Environment2.py:53-134).  Here
+`num_worlds` independent worlds advance together through the HIP kernel of
+wab_gym_amd/csrc/wab_torus.hip (C-ABI include/wab_torus.h):
+
+    env = BatchedWABEnvironment2(32, 32, num_ostriches=1, num_wolves=8, num_bushes=16,
+                                 num_worlds=65536)
+    env.reset_environment()
+    obs, reward, done, info = env.step(actions)    # actions [B, N] int8: one turn of every
+                                                   # world, entities in id order
+    env.get_obs(world, entity, obs)                # the reference's get_obs() result, decoded
+
+`obs` is [B, N, R] uint8 records (include/wab_torus.h): record [b, i] is what entity i's
+`get_obs()` returned in world b at its place in the turn (after entities < i acted), i.e. the
+observation its action of this turn was taken on in the reference's own loop (Env2Tests.py:40-88).
+`fields(obs)` gives typed views of the record fields.  Entities are ostriches, then wolves,
+then bushes (ids in that order, as Env2Tests.py creates them).
+
+Batched-surface conventions (the reference never resets by itself): with `autoreset=True` a
+world in which every ostrich is done after a turn, or whose turn count reached
+`game_options["max_turns"]`, is reset at the end of that turn (`info["world_reset"]`).  Random
+draws are keyed by (seed, world id, episode, what is drawn) instead of Python's global
+`random` stream ("The torus world").
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .torus_options import make_config
+
+TYPES = ("Ostrich", "Wolf", "Bush")
+
+
+class BatchedWABEnvironment2:
+    def __init__(self, world_width=32, world_height=32, game_options=None, num_ostriches=1,
+                 num_wolves=8, num_bushes=16, num_worlds=4096, seed=0x5EED, device="cuda",
+                 world_id_base=0, autoreset=True):
+        import torch
+
+        self._torch = torch
+        lib = _lib.load()
+        self.cfg, self.game_options = make_config(world_width, world_height, num_ostriches, num_wolves,
+                                                  num_bushes, game_options, autoreset)
+        self.width, self.height = int(world_width), int(world_height)
+        self.num_ostriches, self.num_wolves, self.num_bushes = (int(num_ostriches), int(num_wolves),
+                                                                int(num_bushes))
+        self.N = self.num_ostriches + self.num_wolves + self.num_bushes
+        self.num_worlds = int(num_worlds)
+        self.seed = int(seed)
+        self.world_id_base = int(world_id_base)
+        self.autoreset = bool(autoreset)
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("BatchedWABEnvironment2 runs on a HIP device (device='cuda[:i]')")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.R = lib.wab2_record_size(ctypes.addressof(self.cfg))
+        _lib.check2(self.R if self.R < 0 else 0, "wab2_record_size")
+        h = ctypes.c_void_p()
+        _lib.check2(lib.wab2_create(ctypes.addressof(self.cfg), self.num_worlds, self.seed,
+                                    self.world_id_base, dev.index, ctypes.byref(h)), "wab2_create")
+        self._h = h
+        B, N = self.num_worlds, self.N
+        self.obs = torch.zeros((B, N, self.R), dtype=torch.uint8, device=dev)
+        self.reward = torch.zeros((B, N), dtype=torch.float32, device=dev)
+        self.done = torch.zeros((B, N), dtype=torch.uint8, device=dev)
+        self.world_reset = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.types = [TYPES[0]] * self.num_ostriches + [TYPES[1]] * self.num_wolves + [TYPES[2]] * self.num_bushes
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().wab2_destroy(h)
+            except Exception:  # noqa: BLE001 (interpreter shutdown)
+                pass
+            self._h = None
+
+    def _stream(self):
+        return ctypes.c_void_p(self._torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _actions(self, actions, shape):
+        t = self._torch
+        a = actions if isinstance(actions, t.Tensor) else t.as_tensor(np.asarray(actions))
+        if tuple(a.shape) != shape:
+            raise ValueError("actions must have shape %s, got %s" % (shape, tuple(a.shape)))
+        if a.dtype != t.int8:
+            if a.dtype.is_floating_point:
+                raise ValueError("actions must be integers")
+            lo, hi = (int(a.min()), int(a.max())) if a.numel() else (0, 0)
+            if lo < -128 or hi > 127:
+                raise ValueError("actions must fit int8 (the act functions ignore every value "
+                                 "outside 0..5 alike)")
+            a = a.to(t.int8)
+        return a.to(self.device).contiguous()
+
+    # ------------------------------------------------------------------ the reference surface
+    def reset_environment(self, mask=None):
+        """WAB_Environment2.reset_environment (:113-118) of every world, or of the masked ones."""
+        t = self._torch
+        m = None
+        if mask is not None:
+            m = t.as_tensor(mask).to(device=self.device, dtype=t.uint8).contiguous()
+            if tuple(m.shape) != (self.num_worlds,):
+                raise ValueError("mask must have shape (%d,)" % self.num_worlds)
+        _lib.check2(_lib.load().wab2_reset(self._h, None if m is None else m.data_ptr(), self._stream()),
+                    "wab2_reset")
+        self._keep = m
+
+    def step(self, actions):
+        """One turn of every world: for entity i = 0..N-1, get_obs(i) then take_action(i, a[:, i])
+        (WAB_Environment2.py:120-134).  Returns (obs [B, N, R] u8 records, reward [B, N] f32,
+        done [B, N] bool, {"world_reset": [B] bool}); the buffers are the env's own and the
+        next call overwrites them."""
+        a = self._actions(actions, (self.num_worlds, self.N))
+        _lib.check2(_lib.load().wab2_step(self._h, a.data_ptr(), self.obs.data_ptr(), self.reward.data_ptr(),
+                                          self.done.data_ptr(), self.world_reset.data_ptr(), self._stream()),
+                    "wab2_step")
+        return self.obs, self.reward, self.done.bool(), {"world_reset": self.world_reset.bool()}
+
+    def rollout(self, actions):
+        """T turns in one launch: actions [T, B, N] -> (obs [T, B, N, R], reward [T, B, N],
+        done [T, B, N] u8, world_reset [T, B] u8); bit for bit T step() calls."""
+        t = self._torch
+        T = int(actions.shape[0])
+        a = self._actions(actions, (T, self.num_worlds, self.N))
+        B, N = self.num_worlds, self.N
+        obs = t.empty((T, B, N, self.R), dtype=t.uint8, device=self.device)
+        rew = t.empty((T, B, N), dtype=t.float32, device=self.device)
+        done = t.empty((T, B, N), dtype=t.uint8, device=self.device)
+        wr = t.empty((T, B), dtype=t.uint8, device=self.device)
+        _lib.check2(_lib.load().wab2_rollout(self._h, a.data_ptr(), T, obs.data_ptr(), rew.data_ptr(),
+                                             done.data_ptr(), wr.data_ptr(), self._stream()), "wab2_rollout")
+        return obs, rew, done, wr
+
+    # ------------------------------------------------------------------ decoding
+    def fields(self, obs):
+        """Typed views of records [..., N, R]: food f64, x/y i32, visible u32 (bit j: entity j
+        is a row of the frame), flag/status/type u8, delta i8 [..., N, N, 2], bush_food u8
+        [..., N, NB]."""
+        N, NB, R = self.N, self.num_bushes, self.R
+        f = {}
+        f["food"] = obs[..., 0:8].contiguous().view(self._torch.float64)[..., 0]
+        f["x"] = obs[..., 8:12].contiguous().view(self._torch.int32)[..., 0]
+        f["y"] = obs[..., 12:16].contiguous().view(self._torch.int32)[..., 0]
+        f["visible"] = obs[..., 16:20].contiguous().view(self._torch.int32)[..., 0]
+        f["flag"], f["status"], f["type"] = obs[..., 20], obs[..., 21], obs[..., 22]
+        f["delta"] = obs[..., 24:24 + 2 * N].contiguous().view(self._torch.int8).reshape(obs.shape[:-1] + (N, 2))
+        f["bush_food"] = obs[..., 24 + 2 * N:24 + 2 * N + NB]
+        del R
+        return f
+
+    def get_obs(self, world, entity, obs=None):
+        """The reference's get_obs(entity) (World.get_observations, World.py:360-377) of one
+        world, decoded from a record: [rows, internal obs] with rows = [(index, Delta_X, Delta_Y,
+        Type, Additional_Data)] in id order (the visible-objects frame after reset_index) and
+        internal = [x, y, food, role, status] (ostrich), [x, y, food, is_running, status]
+        (wolf) or [x, y, food] (bush)."""
+        rec = (self.obs if obs is None else obs)[world, entity].cpu().numpy()
+        return decode_record(rec, self.types, self.num_bushes)
+
+    def state(self):
+        """Hidden state (synchronising): frame X/Y, object x/y, food, Visible, ostrich status,
+        turn, episode."""
+        B, N = self.num_worlds, self.N
+        s = dict(df_xy=np.zeros((B, N, 2), np.int32), obj_xy=np.zeros((B, N, 2), np.int32),
+                 food=np.zeros((B, N), np.float64), visible=np.zeros((B, N), np.uint8),
+                 status=np.zeros((B, max(self.num_ostriches, 1)), np.uint8), turn=np.zeros(B, np.int32),
+                 episode=np.zeros(B, np.uint32))
+        p = [s[k].ctypes.data for k in ("df_xy", "obj_xy", "food", "visible", "status", "turn", "episode")]
+        _lib.check2(_lib.load().wab2_get_state(self._h, *p, self._stream()), "wab2_get_state")
+        return s
+
+    def counters(self):
+        c = _lib.Wab2Counters()
+        _lib.check2(_lib.load().wab2_get_counters(self._h, ctypes.byref(c), self._stream()), "wab2_get_counters")
+        return {"turns": int(c.turns), "resets": int(c.resets)}
+
+
+def decode_record(rec, types, n_bushes):
+    """One record (uint8 [R]) -> [rows, internal obs] as the reference's get_obs returns them."""
+    rec = np.asarray(rec, dtype=np.uint8)
+    N = len(types)
+    vis = int(rec[16:20].view(np.uint32)[0])
+    dl = rec[24:24 + 2 * N].view(np.int8)
+    bf = rec[24 + 2 * N:24 + 2 * N + n_bushes]
+    bush0 = N - n_bushes
+    rows = []
+    for j in range(N):
+        if vis >> j & 1:
+            extra = [int(bf[j - bush0])] if types[j] == "Bush" else []
+            rows.append((j, int(dl[2 * j]), int(dl[2 * j + 1]), types[j], extra))
+    food = float(rec[0:8].view(np.float64)[0])
+    x, y = int(rec[8:12].view(np.int32)[0]), int(rec[12:16].view(np.int32)[0])
+    t = TYPES[int(rec[22])]
+    if t == "Ostrich":
+        internal = [x, y, food, int(rec[20]), int(rec[21])]
+    elif t == "Wolf":
+        internal = [x, y, food, bool(rec[20]), int(rec[21])]
+    else:
+        internal = [x, y, food]
+    return [rows, internal]
