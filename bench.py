@@ -1,6 +1,6 @@
 """Benchmark: batched Wolves-and-Bushes env-steps/s on MI355X (BASELINE.json `metric`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config default|wide31|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config default|wide31|c5|torus]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A step = one fused pass over all B envs of a rank: move, wolves, bushes, kill/eat/starve,
@@ -119,6 +119,382 @@ def featurize_alg_bytes(W, H, F):
 
 # wab_discounted_returns per env-step: reads reward f32 + done u8, writes the f32 return
 RETURNS_ALG_BYTES = 9
+
+# The Environment 2.0 torus world (include/wab_torus.h): BASELINE config 3's
+# literal reading.  A step is one turn of a world: every entity's get_obs() then take_action()
+# (WAB_Environment2.py:120-134), in id order.
+TORUS = {"width": 32, "height": 32, "counts": (1, 8, 16),
+         "desc": "batch=65536 worlds x Environment 2.0 torus 32x32, 1 ostrich / 8 wolves / 16 bushes "
+                 "(BASELINE config 3 read literally), uniform random actions (ostrich 0..5, wolf 0..4, "
+                 "bush 0), autoreset (every ostrich done or 80 turns)"}
+
+
+def torus_state_bytes(NO, NW, NB):
+    """Per-world state of the torus kernel: own x, y i32 and frame X|Y u16 per entity, food f64
+    per ostrich and wolf, food u8 per bush, the ostrich state byte, turn and episode."""
+    N = NO + NW + NB
+    return 10 * N + 8 * (NO + NW) + NB + NO + 8
+
+
+def torus_alg_bytes(NO, NW, NB, T):
+    """Per world-turn of a T-turn wab2_rollout launch: the N actions, N records of
+    24 + 2N + NB bytes (padding to 16 not counted), reward f32 and done u8 per entity, the
+    world_reset byte, and 2 x state / T."""
+    N = NO + NW + NB
+    return N + N * (24 + 2 * N + NB) + 5 * N + 1 + 2.0 * torus_state_bytes(NO, NW, NB) / T
+
+
+def torus_actions(T, B, NO, NW, NB, dev, gen):
+    """Uniform random actions [T, B, N] int8 on device: ostrich 0..5, wolf 0..4 (Env2Tests.py:27-36
+    draws randint(0, 5) / randint(0, 4)), bush 0."""
+    import torch
+
+    N = NO + NW + NB
+    hi = torch.tensor([6] * NO + [5] * NW + [1] * NB, dtype=torch.int32, device=dev)
+    out = torch.empty((T, B, N), dtype=torch.int8, device=dev)
+    for t0 in range(0, T, 16):
+        t1 = min(T, t0 + 16)
+        r = torch.randint(0, 1 << 30, (t1 - t0, B, N), device=dev, generator=gen, dtype=torch.int32)
+        out[t0:t1] = (r % hi).to(torch.int8)
+    return out
+
+
+def time_launches(launch, n, dev, stream, mode="graph", min_seconds=MIN_TIMED_SECONDS):
+    """Average duration of one of `n` back-to-back launches (launch(i, hip_stream)), captured in a
+    graph as the timed region is, replayed until at least `min_seconds` are timed; HIP events on
+    the launch stream.  Returns (ms per launch, launches timed)."""
+    import torch
+
+    def launches(st):
+        sc = ctypes.c_void_p(st.cuda_stream)
+        for i in range(n):
+            launch(i, sc)
+    g = None
+    if mode == "graph":
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                launches(torch.cuda.current_stream(dev))
+        stream.wait_stream(side)
+
+    def once():
+        if g is not None:
+            g.replay()
+        else:
+            launches(stream)
+    once()  # warm
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    once()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    reps = window_replays(e0.elapsed_time(e1) * 1e-3, min_seconds)
+    e0.record(stream)
+    for _ in range(reps):
+        once()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / (reps * n), reps * n
+
+
+def torus_cpu_baseline(seconds, threads):
+    """oracle/wab_torus_oracle.c (the scalar restatement of World.py's turn) on this host's
+    cores, a bounded sample of the same workload."""
+    import numpy as np
+
+    from oracle.torus_oracle import OracleTorus
+
+    NO, NW, NB = TORUS["counts"]
+    Bc = 2048
+    orc = OracleTorus(TORUS["width"], TORUS["height"], NO, NW, NB, batch=Bc)
+    orc.reset()
+    rng = np.random.RandomState(0)
+    hi = np.array([6] * NO + [5] * NW + [1] * NB)
+    acts = [(rng.randint(0, 1 << 30, size=(Bc, NO + NW + NB)) % hi).astype(np.int8) for _ in range(32)]
+    orc.step(acts[0], nthreads=threads)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        orc.step(acts[n % 32], nthreads=threads)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(Bc * n / el, 1), "unit": "env-steps/s (world-turns)", "cores": threads, "kind": "port",
+            "sample": "oracle/wab_torus_oracle.c turn, %d worlds x %d turns (%.1f s) of the same workload%s"
+                      % (Bc, n, el, ", OpenMP over worlds" if threads > 1 else ", 1 thread")}
+
+
+def roofline_entry(alg, us_per_step, B, traffic_key=None, kernel=None, steps_per_launch=1):
+    """The roofline object of a `configs` entry: algorithmic bytes per env-step x B over the
+    measured time per step, against the HBM peak; traffic from the committed PMC summary."""
+    achieved = alg * B / (us_per_step * 1e-6) / 1e9
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "alg_bytes_per_env_step": round(alg, 3),
+           "alg_bytes_per_launch": round(alg * B * steps_per_launch), "kernel": kernel}
+    traffic, src = committed_traffic(traffic_key, B) if traffic_key else (None, None)
+    out["traffic"] = None if traffic is None else round(traffic)
+    out["traffic_unit"] = "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE, committed profile)"
+    out["traffic_source"] = src
+    return out
+
+
+def extra_configs(args, dev, B):
+    """The other BASELINE configs and surfaces, timed beside the headline on the same GPU (rank 0
+    of a 1-GPU run): C3's wide rollout and its per-step launch into a 32-slot obs ring, C5's
+    wab_rollout_features, the default per-step launch into a ring, and the Environment 2.0
+    torus world.  Each: reset, >= 2 x max_turns untimed steps, then >= 32 launches and >= 0.2 s
+    timed (time_launches)."""
+    import torch
+
+    from wab_gym_amd import _lib
+    from wab_gym_amd.env import BatchedWolvesAndBushesEnv
+    from wab_gym_amd.torus import BatchedWABEnvironment2
+
+    L = _lib.load()
+    stream = torch.cuda.current_stream(dev)
+    T = DEFAULT_ROLLOUT
+    out = {}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4321)
+    NL = MIN_TIMED_LAUNCHES
+
+    def entry(us, alg, key, kernel, spl, n, api):
+        return {"api": api, "us_per_step": round(us, 3), "env_steps_per_s": round(B / (us * 1e-6), 1),
+                "launches_timed": n, "steps_per_launch": spl,
+                "roofline": roofline_entry(alg, us, B, key, kernel, spl)}
+
+    for cfg in ("wide31", "c5", "default"):
+        opts, stride, slots, _ = CONFIGS[cfg]
+        env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev, autoreset=True,
+                                        validate_actions=False, plane_stride=stride, wolf_slots=slots)
+        h, W = env._h, 2 * int(env.game_options["max_turns"])
+        W = -(-W // T) * T
+        acts = torch.randint(0, env.n_actions, (W + NL * T, B), device=dev, generator=gen).to(torch.int8)
+        a0 = acts.data_ptr()
+        env.reset()
+        if cfg == "c5":
+            F = int(L.wab_feature_dim(h))
+            feats = torch.empty((T, B, F), dtype=torch.float32, device=dev)
+            rd = torch.empty((T, B), dtype=torch.float32, device=dev)
+            dn = torch.empty((T, B), dtype=torch.uint8, device=dev)
+            ret = torch.empty((T, B), dtype=torch.float32, device=dev)
+            sc = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
+            rseq = _lib.WabObs(None, sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
+
+            def roll(t, s):
+                _lib.check(L.wab_rollout_features(h, a0 + t * B, T, ctypes.addressof(rseq), rd.data_ptr(),
+                                                  dn.data_ptr(), feats.data_ptr(), 0.99, None, ret.data_ptr(), s),
+                           "wab_rollout_features")
+            for t in range(0, W, T):
+                roll(t, ctypes.c_void_p(stream.cuda_stream))
+            ms, n = time_launches(lambda i, s: roll(W + i * T, s), NL, dev, stream, args.mode)
+            out["c5_rollout"] = entry(ms * 1e3 / T, c5_rollout_alg_bytes(F, T), "c5_rollout%d" % T,
+                                      "wab_step_small + features + returns, rollout build (wab_rollout_features)",
+                                      T, n, "wab_rollout_features, %d steps per launch (C5: actor_critic.py:185-200)" % T)
+            del feats
+        else:
+            pl = torch.empty((T, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+            sc = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
+            rd = torch.empty((T, B), dtype=torch.float32, device=dev)
+            dn = torch.empty((T, B), dtype=torch.uint8, device=dev)
+            seq = _lib.WabObs(pl.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
+
+            def roll(t, s):
+                _lib.check(L.wab_rollout(h, a0 + t * B, T, ctypes.addressof(seq), rd.data_ptr(), dn.data_ptr(), s),
+                           "wab_rollout")
+            for t in range(0, W, T):
+                roll(t, ctypes.c_void_p(stream.cuda_stream))
+            kname = "wab_step_%s" % L.wab_step_kernel(h).decode()
+            if cfg == "wide31":
+                ms, n = time_launches(lambda i, s: roll(W + i * T, s), NL, dev, stream, args.mode)
+                out["wide31_rollout"] = entry(ms * 1e3 / T, alg_bytes_per_env_step_rollout(env.W, env.H, T),
+                                              "wide31_rollout%d" % T, kname + ", rollout build", T, n,
+                                              "wab_rollout, %d steps per launch (C3: 31x31 in 32x32 planes)" % T)
+            # the per-step surface: one wab_step launch per step, step t's obs into slot t % 32
+            # of a ring of [B] buffers (so they reach HBM as a closed loop's would)
+            del pl
+            NR = 32
+            rp = torch.empty((NR, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+            rs = torch.empty((3, NR, B), dtype=torch.uint8, device=dev)
+            rr = torch.empty((NR, B), dtype=torch.float32, device=dev)
+            rdn = torch.empty((NR, B), dtype=torch.uint8, device=dev)
+            slots_ = [_lib.WabObs(rp[i].data_ptr(), rs[0, i].data_ptr(), rs[1, i].data_ptr(), rs[2, i].data_ptr())
+                      for i in range(NR)]
+            _lib.check(L.wab_set_obs_placement(h, _lib.OBS_FRESH_BUFFER), "wab_set_obs_placement")
+            ms, n = time_launches(lambda i, s: _lib.check(L.wab_step(h, a0 + (W + i % (NL * T)) * B,
+                                                                     ctypes.addressof(slots_[i % NR]),
+                                                                     rr[i % NR].data_ptr(), rdn[i % NR].data_ptr(),
+                                                                     None, s), "wab_step"),
+                                  256, dev, stream, args.mode)
+            out["%s_per_step_ring" % cfg] = entry(
+                ms * 1e3, alg_bytes_per_env_step(env.W, env.H), "%s_ring%d" % (cfg, NR), kname, 1, n,
+                "wab_step (the raw C-ABI per-step launch), step t's obs into slot t %% %d of a ring of [B] "
+                "buffers" % NR)
+            del rp
+        del env, acts
+        torch.cuda.empty_cache()
+    # the Environment 2.0 torus world (SURVEY.md §8 f4)
+    NO, NW, NB = TORUS["counts"]
+    tenv = BatchedWABEnvironment2(TORUS["width"], TORUS["height"], None, NO, NW, NB, num_worlds=B, seed=0x5EED,
+                                  device=dev)
+    N, R, h = tenv.N, tenv.R, tenv._h
+    W = -(-2 * int(tenv.game_options["max_turns"]) // T) * T
+    acts = torus_actions(W + NL * T, B, NO, NW, NB, dev, gen)
+    ob = torch.empty((T, B, N, R), dtype=torch.uint8, device=dev)
+    rw = torch.empty((T, B, N), dtype=torch.float32, device=dev)
+    dn = torch.empty((T, B, N), dtype=torch.uint8, device=dev)
+    wr = torch.empty((T, B), dtype=torch.uint8, device=dev)
+
+    def troll(t, s):
+        _lib.check2(L.wab2_rollout(h, acts.data_ptr() + t * B * N, T, ob.data_ptr(), rw.data_ptr(), dn.data_ptr(),
+                                   wr.data_ptr(), s), "wab2_rollout")
+    tenv.reset_environment()
+    for t in range(0, W, T):
+        troll(t, ctypes.c_void_p(stream.cuda_stream))
+    ms, n = time_launches(lambda i, s: troll(W + i * T, s), NL, dev, stream, args.mode)
+    e = entry(ms * 1e3 / T, torus_alg_bytes(NO, NW, NB, T), "torus_rollout%d" % T,
+              "wab_torus_kernel (%d turns per launch)" % T, T, n,
+              "wab2_rollout, %d turns per launch (Environment 2.0 torus 32x32, 1/8/16)" % T)
+    e["entity_actions_per_s"] = round(e["env_steps_per_s"] * N, 1)
+    out["torus_rollout"] = e
+    del tenv, ob, acts
+    torch.cuda.empty_cache()
+    return out
+
+
+def run_torus(args, dev, rank, world):
+    """bench.py --config torus: T-turn wab2_rollout launches of B worlds per rank."""
+    import torch
+    import torch.distributed as dist
+
+    from wab_gym_amd.shard import all_gather_objects, env_id_base, max_over_ranks
+    from wab_gym_amd.torus import BatchedWABEnvironment2
+
+    NO, NW, NB = TORUS["counts"]
+    B, T = args.batch, (args.rollout if args.rollout > 0 else DEFAULT_ROLLOUT)
+    env = BatchedWABEnvironment2(TORUS["width"], TORUS["height"], None, NO, NW, NB, num_worlds=B,
+                                 seed=0x5EED, device=dev, world_id_base=env_id_base(rank, B))
+    N, R = env.N, env.R
+    W = max(args.warmup, 2 * int(env.game_options["max_turns"]))
+    W = -(-W // T) * T
+    K = window_steps(args.steps, T)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    actions = torus_actions(W + K, B, NO, NW, NB, dev, gen)
+    obs = torch.empty((T, B, N, R), dtype=torch.uint8, device=dev)
+    rew = torch.empty((T, B, N), dtype=torch.float32, device=dev)
+    done = torch.empty((T, B, N), dtype=torch.uint8, device=dev)
+    wr = torch.empty((T, B), dtype=torch.uint8, device=dev)
+    from wab_gym_amd import _lib
+    L, h = _lib.load(), env._h
+    a0, o0, r0, d0, w0 = actions.data_ptr(), obs.data_ptr(), rew.data_ptr(), done.data_ptr(), wr.data_ptr()
+
+    def run(t0, n, stream):
+        s = ctypes.c_void_p(stream.cuda_stream)
+        for t in range(t0, t0 + n, T):
+            _lib.check2(L.wab2_rollout(h, a0 + t * B * N, T, o0, r0, d0, w0, s), "wab2_rollout")
+
+    stream = torch.cuda.current_stream(dev)
+    env.reset_environment()
+    run(0, W, stream)
+    torch.cuda.synchronize(dev)
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(stream)
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            run(W, K, torch.cuda.current_stream(dev))
+    stream.wait_stream(side)
+    torch.cuda.synchronize(dev)
+    env.reset_environment()  # the capture did not execute the turns: rewind
+    run(0, W, stream)
+    torch.cuda.synchronize(dev)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record(stream)
+    graph.replay()
+    c1.record(stream)
+    torch.cuda.synchronize(dev)
+    reps = window_replays(c0.elapsed_time(c1) * 1e-3)
+    if world > 1:
+        reps = int(max_over_ranks(reps))
+    cb = env.counters()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_wall = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(reps):
+        graph.replay()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t_wall
+    stream_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(stream_ms * 1e-3)
+    ca = env.counters()
+    steps = K * reps
+    kern_ms = stream_ms / steps  # per turn (launch / T)
+    alg = torus_alg_bytes(NO, NW, NB, T)
+    # the per-step surface beside it: one wab2_step launch per turn, records into a 32-slot ring
+    NR = 32
+    ring = torch.empty((NR, B, N, R), dtype=torch.uint8, device=dev)
+    ring_rd = torch.empty((NR, B, N), dtype=torch.float32, device=dev)
+    ring_dn = torch.empty((NR, B, N), dtype=torch.uint8, device=dev)
+    ps_ms, ps_n = time_launches(
+        lambda i, s: _lib.check2(L.wab2_step(h, a0 + (W + i) * B * N, ring[i % NR].data_ptr(),
+                                             ring_rd[i % NR].data_ptr(), ring_dn[i % NR].data_ptr(), None, s),
+                                 "wab2_step"), min(K, 256), dev, stream, args.mode)
+    del ring
+    ps_alg = torus_alg_bytes(NO, NW, NB, 1)
+    achieved = alg * B / (kern_ms * 1e-3) / 1e9
+    per_rank = all_gather_objects({"rank": rank, "device": str(dev), "pci": pci_id(dev),
+                                   "env_steps_per_s": round(B * steps / (stream_ms * 1e-3), 1),
+                                   "stream_ms": round(stream_ms, 3), "achieved_GBs": round(achieved, 1)})
+    if rank == 0:
+        traffic, traffic_src = committed_traffic("torus_rollout%d" % T, B)
+        line = {
+            "metric": METRIC, "value": round(world * B * steps / elapsed, 1), "unit": "env-steps/s",
+            "n_gpus": world, "steps": steps, "steps_requested": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / steps, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: uniform random actions (torch.randint on device), keyed-RNG worlds",
+            "config": {"workload": TORUS["desc"] + "; %d-turn wab2_rollout launches (records, reward, done "
+                                                   "of every turn into [%d, B] buffers)" % (T, T),
+                       "batch_per_gpu": B, "global_batch": B * world, "world": [TORUS["width"], TORUS["height"]],
+                       "entities": {"ostriches": NO, "wolves": NW, "bushes": NB}, "record_bytes": R,
+                       "launch": args.mode, "parallelism": "independent world shards x%d (no collective)" % world},
+            "entity_actions_per_s": round(world * B * steps * N / elapsed, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)", "traffic_source": traffic_src,
+                         "alg_bytes_per_launch": round(alg * B * T), "kernel": "wab_torus_kernel (%d turns per launch)" % T,
+                         "kernel_us": round(kern_ms * T * 1e3, 3), "alg_bytes_per_env_step": round(alg, 3)},
+            "per_step_launch": {"api": "wab2_step, records into a %d-slot ring of [B, N, R] buffers" % NR,
+                                "us_per_step": round(ps_ms * 1e3, 3),
+                                "env_steps_per_s": round(B / (ps_ms * 1e-3), 1),
+                                "alg_bytes_per_env_step": round(ps_alg, 3),
+                                "frac": round(ps_alg * B / (ps_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "timed_window": {"turns": ca["turns"] - cb["turns"], "resets": ca["resets"] - cb["resets"],
+                             "graph_steps": K, "graph_replays": reps, "launches": steps // T,
+                             "stream_ms": round(stream_ms, 3), "wall_ms": round(wall * 1e3, 3),
+                             "floor": {"min_launches": MIN_TIMED_LAUNCHES, "min_seconds": MIN_TIMED_SECONDS}},
+            "warmup_effective": W,
+            "devices": sorted({r["pci"] for r in per_rank}),
+        }
+        if world > 1:
+            line["per_rank"] = per_rank
+        if world == 1 and not args.no_cpu:
+            cores = host_cores()
+            line["cpu_baseline"] = torus_cpu_baseline(args.cpu_seconds, cores["used"])
+            line["cpu_baseline"]["host"] = cores
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def host_cores():
@@ -285,7 +661,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="default", choices=sorted(CONFIGS) + ["torus"])
     ap.add_argument("--mode", default="graph", choices=["graph", "launch"])
     ap.add_argument("--rollout", type=int, default=-1,
                     help="T > 0: wab_rollout (c5: wab_rollout_features) segments of T steps (one "
@@ -298,6 +674,8 @@ def main():
                          "[B] buffer rewritten every step (which a 256 MB Infinity Cache can absorb)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="default config: skip the other configs' lines (configs key) timed beside it")
     ap.add_argument("--no-diag", action="store_true",
                     help="skip the diagnostic launches beside the line (per-step launches, single-launch "
                          "timings): for profiling the line's kernel alone")
@@ -343,6 +721,9 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("gloo")  # CPU only: barrier + timing MAX; no RCCL
+
+    if args.config == "torus":
+        return run_torus(args, dev, rank, world)
 
     from wab_gym_amd import _lib
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
@@ -465,6 +846,7 @@ def main():
         ring_slots = [_lib.WabObs(ring_planes[i].data_ptr(), ring_scal[0, i].data_ptr(), ring_scal[1, i].data_ptr(),
                              ring_scal[2, i].data_ptr()) for i in range(N)]
         slot_addr = [ctypes.addressof(o) for o in ring_slots]
+        _lib.check(L.wab_set_obs_placement(h, _lib.OBS_FRESH_BUFFER), "wab_set_obs_placement")
 
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
@@ -612,18 +994,22 @@ def main():
         ring_addr = [ctypes.addressof(o) for o in ring_obs]
         rr = torch.empty((NR, B), dtype=torch.float32, device=dev)
         n_ps = min(K_req, 512)
+        _lib.check(L.wab_set_obs_placement(h, _lib.OBS_FRESH_BUFFER), "wab_set_obs_placement")
         ps_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, ring_addr[i % NR], rr[i % NR].data_ptr(),
                                                    ring_rd[i % NR].data_ptr(), None, s), n_ps)
+        _lib.check(L.wab_set_obs_placement(h, _lib.OBS_SAME_BUFFER), "wab_set_obs_placement")
         psc_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_ps)
         del ring_planes
         roll_line = {"steps_per_launch": T_roll, "launch_us": round(kern_ms * T_roll * 1e3, 3),
-                     "per_step_launch": {"api": "wab_step (BatchedWolvesAndBushesEnv.step), obs into a "
-                                                "%d-slot ring of [B] buffers" % NR,
+                     "per_step_launch": {"api": "wab_step (the raw C-ABI per-step launch), step t's obs into "
+                                                "slot t %% %d of a ring of [B] buffers" % NR,
                                          "us_per_step": round(ps_ms * 1e3, 3),
                                          "env_steps_per_s": round(B / (ps_ms * 1e-3), 1),
                                          "alg_bytes_per_env_step": alg,
                                          "frac": round(alg * B / (ps_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                         "one_buffer_us_per_step": round(psc_ms * 1e3, 3)}}
+                                         # BatchedWolvesAndBushesEnv.step's own pattern: every step
+                                         # into the env's one [B] obs buffer (Infinity-Cache resident)
+                                         "env_step_one_buffer_us_per_step": round(psc_ms * 1e3, 3)}}
         alg = alg_bytes_per_env_step_rollout(env.W, env.H, T_roll)
         kernel_name = "wab_step_%s, rollout build (%d steps per launch)" % (L.wab_step_kernel(h).decode(), T_roll)
     if c5:
@@ -762,6 +1148,10 @@ def main():
             line["rollout"] = roll_line
         else:
             line["roofline"]["kernel_us_single_launch_median"] = round(single_ms * 1e3, 3)
+        if world == 1 and args.config == "default" and rollout and not args.no_extra:
+            # C3, C5, the per-step surfaces and the torus world beside the headline (their own
+            # roofline each; the headline fields above are the default config's alone)
+            line["configs"] = extra_configs(args, dev, B)
         if world == 1 and not args.no_cpu:
             cores = host_cores()
             line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, cores["used"], c5)

@@ -197,6 +197,23 @@ int wab_get_state(wab_handle* h, double* food, int32_t* x, int32_t* y, int32_t* 
 /* Batch size of a handle. */
 int64_t wab_batch(const wab_handle* h);
 
+/* Where the caller's wab_step observations go, a performance hint with no effect on results
+ * (default WAB_OBS_SAME_BUFFER):
+ *   WAB_OBS_SAME_BUFFER   every step into the same obs buffer (the env's own, as
+ *                         BatchedWolvesAndBushesEnv.step does): the per-step kernel, which stores
+ *                         each plane as soon as it is final (a 128-byte line at a plane or env
+ *                         boundary written in two parts, which the Infinity Cache merges when the
+ *                         buffer stays resident);
+ *   WAB_OBS_FRESH_BUFFER  each step into a buffer the last steps did not write (a closed loop's
+ *                         ring of obs slots): on the wide kernel (wab_step_kernel "wide"), without
+ *                         terminal obs, a one-step launch of its rollout build, which stores whole
+ *                         lines in address order after the step (C3 at B = 65536: 52 us per step
+ *                         into a 32-slot ring, against 73 us for the per-step kernel).
+ * Other kernels ignore it.  Host only, no synchronisation. */
+#define WAB_OBS_SAME_BUFFER 0
+#define WAB_OBS_FRESH_BUFFER 1
+int wab_set_obs_placement(wab_handle* h, int32_t placement);
+
 /* Name of the kernel wab_step launches for this handle: "small" (the four-wave kernel for
  * views of at most 128 cells in unpadded rows), "wide" (views of at most 32x32 cells in rows
  * of 16 or 32 bytes, without restrict_view: the 31x31 configuration) or "block" (the general

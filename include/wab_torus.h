@@ -24,6 +24,8 @@
  *                        (World.get_observations :360-377, perform_entity_action :325-334,
  *                        default_game_update :93-132)
  *   wab2_rollout      <- T turns of the same
+ *   wab2_get_obs      <- get_obs(entity_id)                             WAB_Environment2.py:120-123
+ *   wab2_take_action  <- take_action(entity_id, action) -> (reward, done) WAB_Environment2.py:125-134
  *   wab2_obs record   <- get_obs(i): [visible-objects frame, internal obs] World.py:243-323
  *
  * Randomness: every draw is Python's random.randint in the reference; here it is keyed
@@ -145,6 +147,22 @@ int wab2_step(wab2_handle* h, const int8_t* actions, uint8_t* obs, float* reward
  * (or NULL): bit for bit T wab2_step calls, in ONE launch (state on chip between turns). */
 int wab2_rollout(wab2_handle* h, const int8_t* actions, int32_t T, uint8_t* obs, float* reward,
                  uint8_t* done, uint8_t* world_reset, void* stream);
+
+/* The reference's per-entity calls, batched over the worlds (WAB_Environment2.py:120-134; the
+ * loop of Env2Tests.py:40-88): each world's entity `entity` observes, then acts, in id order.
+ *   wab2_get_obs      obs [B][R]: entity's record in every world as it is now
+ *                     (World.get_observations); any entity that has not acted this turn;
+ *   wab2_take_action  actions [B] int8 -> reward [B] f32, done [B] u8 of that entity
+ *                     (perform_entity_action + is_entity_done); entities act in id order,
+ *                     each once per turn (the reference allows any order; this surface
+ *                     requires ascending ids, so a turn is entities 0..N-1).  The call of
+ *                     entity N-1 ends the turn: World.increment_turn and, with autoreset, the
+ *                     resets (world_reset [B] u8 or NULL, written by every call).
+ * wab2_step / wab2_rollout run whole turns and are refused while a turn is half done;
+ * wab2_reset(mask = NULL) restarts the turn at entity 0, a masked reset only between turns. */
+int wab2_get_obs(wab2_handle* h, int32_t entity, uint8_t* obs, void* stream);
+int wab2_take_action(wab2_handle* h, int32_t entity, const int8_t* actions, float* reward, uint8_t* done,
+                     uint8_t* world_reset, void* stream);
 
 /* Hidden state to HOST arrays (any may be NULL; synchronises `stream`): the frame's X/Y
  * df_xy [B][N][2] i32, the entities' own x/y obj_xy [B][N][2] i32, food [B][N] f64, the

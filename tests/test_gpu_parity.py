@@ -1039,9 +1039,10 @@ def test_rollout_features_ambiguous_rewards_fail_before_stepping():
 
 
 def test_wide_step_into_alternating_buffers():
-    """The wide view's wab_step picks its kernel by the obs buffer (the last step's: the per-step
-    kernel; another: the rollout build with one step): steps alternating between two obs
-    buffers (and back to one) switch kernels every step and still match the oracle bit for bit."""
+    """The wide view's wab_step runs the per-step kernel (WAB_OBS_SAME_BUFFER, the default) or a
+    one-step launch of its rollout build (wab_set_obs_placement(WAB_OBS_FRESH_BUFFER)): steps
+    alternating between two obs buffers, under either placement and switching placement every
+    20 steps, match the oracle bit for bit."""
     import ctypes
 
     import torch
@@ -1057,8 +1058,11 @@ def test_wide_step_into_alternating_buffers():
     assert env.step_kernel == "wide"
     bufs = [env._alloc_obs() for _ in range(2)]
     L = _lib.load()
+    assert L.wab_set_obs_placement(env._h, 7) == -1
     rng = np.random.RandomState(21)
     for t in range(120):
+        if t % 20 == 0:
+            _lib.check(L.wab_set_obs_placement(env._h, (t // 20) % 2), "wab_set_obs_placement")
         a = rng.randint(5, size=n)
         o = bufs[t % 2] if t < 80 else bufs[0]
         ad = torch.as_tensor(a.astype(np.int8), device="cuda:0")

@@ -209,7 +209,7 @@ def test_torus_shard_invariance():
 
 
 def test_torus_decoded_obs_matches_reference_frame():
-    """get_obs() decoded from a record gives the reference's rows and internal obs (golden)."""
+    """frame() decodes a record into the reference's rows and internal obs (golden)."""
     import torch
 
     from wab_gym_amd.torus import decode_record
@@ -217,11 +217,82 @@ def test_torus_decoded_obs_matches_reference_frame():
     d, meta = load_set("torus_multi")
     env = make_env(meta, meta["world_ids"][0])
     env.reset_environment()
-    env.step(torch.as_tensor(d["actions"][0, 0][None]))
+    obs, _, _, _ = env.step(torch.as_tensor(d["actions"][0, 0][None]))
     for i in range(env.N):
-        rows, internal = env.get_obs(0, i)
+        rows, internal = env.frame(obs[0, i])
         assert [rows, internal] == decode_record(d["records"][0, 0, i], env.types, env.num_bushes)
         assert internal[:2] == [int(v) for v in d["reset0_obj_xy"][0, i]]
+
+
+@pytest.mark.parametrize("name", ["torus_multi", "torus_tiny"])
+def test_torus_per_entity_calls_match_reference_golden(name):
+    """get_obs(i) then take_action(i, a) for every entity, the reference's own loop
+    (Env2Tests.py:40-88), in every world at once: the golden records, rewards, dones and resets."""
+    import torch
+
+    d, meta = load_set(name)
+    ids = meta["world_ids"]
+    T = min(meta["T"], 60)
+    envs = [make_env(meta, g) for g in ids]
+    for env in envs:
+        env.reset_environment()
+    N = envs[0].N
+    for t in range(T):
+        for i in range(N):
+            for e, env in enumerate(envs):
+                rec = env.get_obs(i)[0].cpu().numpy()
+                assert np.array_equal(rec, d["records"][t, e, i]), "%s world %d turn %d entity %d" % (name, ids[e], t, i)
+                r, dn, info = env.take_action(i, torch.as_tensor(d["actions"][t, e, i:i + 1]))
+                assert float(r[0]) == d["reward"][t, e, i] and bool(dn[0]) == d["done"][t, e, i]
+                if i == N - 1:
+                    assert bool(info["world_reset"][0]) == bool(d["world_reset"][t, e])
+    for e, env in enumerate(envs):
+        check_state(env, d, T - 1, e, "%s world %d after %d turns of per-entity calls" % (name, ids[e], T))
+
+
+def test_torus_per_entity_order_is_enforced():
+    import torch
+
+    _, meta = load_set("torus_c3")
+    env = make_env(meta, 0, batch=128)
+    env.reset_environment()
+    a = torch.zeros(128, dtype=torch.int8)
+    with pytest.raises(ValueError):
+        env.take_action(1, a)  # entity 0 acts first
+    env.get_obs(3)  # not acted yet: allowed
+    env.take_action(0, a)
+    with pytest.raises(ValueError):
+        env.get_obs(0)  # acted this turn
+    with pytest.raises(ValueError):
+        env.step(torch.zeros((128, env.N), dtype=torch.int8))  # a turn is half done
+    env.reset_environment()  # restarts the turn
+    env.step(torch.zeros((128, env.N), dtype=torch.int8))
+
+
+def test_torus_per_entity_equals_turn_launch_at_scale():
+    """N get_obs + take_action launches per turn == one wab2_step launch, at B = 65536."""
+    import torch
+
+    _, meta = load_set("torus_c3")
+    B = 65536
+    a_env = make_env(meta, 0, batch=B)
+    b_env = make_env(meta, 0, batch=B)
+    a_env.reset_environment()
+    b_env.reset_environment()
+    rng = np.random.RandomState(5)
+    hi = np.array([6] + [5] * 8 + [1] * 16)
+    for t in range(12):
+        acts = torch.as_tensor((rng.randint(0, 1 << 20, size=(B, 25)) % hi).astype(np.int8), device="cuda:0")
+        obs, rew, done, info = a_env.step(acts)
+        for i in range(25):
+            rec = b_env.get_obs(i)
+            assert torch.equal(rec, obs[:, i]), (t, i)
+            r, dn, inf = b_env.take_action(i, acts[:, i].contiguous())
+            assert torch.equal(r, rew[:, i]) and torch.equal(dn, done[:, i]), (t, i)
+        assert torch.equal(inf["world_reset"], info["world_reset"]), t
+    sa, sb = a_env.state(), b_env.state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
 
 
 def test_torus_rejects_bad_options():

@@ -18,13 +18,15 @@ EXPORTED = [
     "wab_feature_dim", "wab_featurize", "wab_discounted_returns", "wab_step_kernel",
     "wab_superbasic_dim", "wab_featurize_superbasic", "wab_render", "wab_egocentric",
     "wab_debug_bush_values", "wab_step_features", "wab_discounted_returns_exact",
-    "wab_bush_thresholds", "wab_rollout_features", "wab_render_envs",
+    "wab_bush_thresholds", "wab_rollout_features", "wab_render_envs", "wab_set_obs_placement",
     # include/wab_torus.h: the Environment 2.0 torus world
     "wab2_abi_version", "wab2_last_error", "wab2_record_size", "wab2_create", "wab2_destroy",
     "wab2_batch", "wab2_reset", "wab2_step", "wab2_rollout", "wab2_get_state", "wab2_get_counters",
+    "wab2_get_obs", "wab2_take_action",
 ]
 
 ABI2_VERSION = 1
+OBS_SAME_BUFFER, OBS_FRESH_BUFFER = 0, 1  # wab_set_obs_placement
 
 ABI_VERSION = 4
 
@@ -89,6 +91,7 @@ def load():
     L.wab_batch.restype = I64
     L.wab_step_kernel.argtypes = [P]
     L.wab_step_kernel.restype = ctypes.c_char_p
+    L.wab_set_obs_placement.argtypes = [P, I32]
     L.wab2_abi_version.restype = ctypes.c_int
     L.wab2_last_error.restype = ctypes.c_char_p
     L.wab2_record_size.argtypes = [P]
@@ -101,6 +104,8 @@ def load():
     L.wab2_rollout.argtypes = [P, P, I32, P, P, P, P, P]
     L.wab2_get_state.argtypes = [P] * 9
     L.wab2_get_counters.argtypes = [P, P, P]
+    L.wab2_get_obs.argtypes = [P, I32, P, P]
+    L.wab2_take_action.argtypes = [P, I32, P, P, P, P, P]
     for name in EXPORTED:
         if name not in ("wab_abi_version", "wab_last_error", "wab_batch", "wab_step_kernel",
                         "wab2_abi_version", "wab2_last_error", "wab2_batch"):

@@ -60,7 +60,7 @@ struct wab_handle {
   wab::RewardTable rewards;  // exact doubles of the rewards a step returns (n = 0: ambiguous)
   size_t wide_lds_bytes = 0;  // LDS per workgroup of the wide kernel (see wab_create)
   size_t wide_roll_lds_bytes = 0;  // ... of its multi-step build (wab_rollout_wide)
-  const uint8_t* last_step_planes = nullptr;  // the obs planes of the last wab_step (wide view)
+  int32_t obs_placement = WAB_OBS_SAME_BUFFER;  // wab_set_obs_placement: which wide per-step build
 };
 
 namespace {
@@ -362,6 +362,15 @@ int64_t wab_batch(const wab_handle* h) { return h ? h->p.B : 0; }
 const char* wab_step_kernel(const wab_handle* h) {
   if (!h) return "";
   return h->step_kernel == KERNEL_SMALL ? "small" : h->step_kernel == KERNEL_WIDE ? "wide" : "block";
+}
+
+int wab_set_obs_placement(wab_handle* h, int32_t placement) {
+  g_err.clear();
+  if (!h) return fail(WAB_E_INVALID, "wab_set_obs_placement: NULL handle");
+  if (placement != WAB_OBS_SAME_BUFFER && placement != WAB_OBS_FRESH_BUFFER)
+    return fail(WAB_E_INVALID, "wab_set_obs_placement: WAB_OBS_SAME_BUFFER or WAB_OBS_FRESH_BUFFER");
+  h->obs_placement = placement;
+  return WAB_OK;
 }
 
 int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id_base, int device,
@@ -678,14 +687,14 @@ int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* re
     p.t_status = terminal->status;
   }
   DeviceGuard guard(h->device);
-  const bool same_buffer = obs->planes == h->last_step_planes;
-  h->last_step_planes = obs->planes;
-  if (h->step_kernel == KERNEL_WIDE && !p.t_planes && !same_buffer && ((size_t)p.B * (size_t)p.OB) % 16u == 0) {
-    // The wide view, without terminal obs, into a different obs buffer than the last step's: the
+  if (h->step_kernel == KERNEL_WIDE && !p.t_planes && h->obs_placement == WAB_OBS_FRESH_BUFFER &&
+      ((size_t)p.B * (size_t)p.OB) % 16u == 0) {
+    // The wide view, without terminal obs, each step into a buffer the last steps did not write
+    // (wab_set_obs_placement(WAB_OBS_FRESH_BUFFER), a closed loop's ring of obs slots): the
     // rollout build with one step (its obs as whole 128-byte lines in address order after the
-    // step).  Into the buffer of the last step (the env's own, rewritten every step, which the
-    // 256 MB Infinity Cache holds) the per-step kernel, which stores each plane as soon as it is
-    // final (a line at a plane or env boundary in two parts, merged on die).  Measured at
+    // step).  Into one buffer rewritten every step (WAB_OBS_SAME_BUFFER, the env's own, which
+    // the 256 MB Infinity Cache holds) the per-step kernel, which stores each plane as soon as it
+    // is final (a line at a plane or env boundary in two parts, merged on die).  Measured at
     // B = 65536 (C3): into a 32-slot ring 52.0 against 73.1 us (round 3's per-step kernel), into
     // one buffer 62.5 against 45.9 us.  The results are the same either way.
     if (h->n_blocks == 0) return WAB_OK;

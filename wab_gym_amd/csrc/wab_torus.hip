@@ -79,8 +79,12 @@ struct TParams {
   int32_t fpb, fg;        // food_per_bush, food_given_per_turn
   double ofood0, wfood0, wff;
   int32_t role0, max_turns, autoreset;
-  uint32_t magic_n;       // ceil(2^20 / N): q / N for q < 2048
   int32_t act_scalar;     // actions may be read with scalar loads (4-byte aligned slices)
+  // the launch's entity windows (a whole turn: both [0, N)): entities [a0, a1) act, in id
+  // order, and the records of observers [o0, o1) are written, each as it observes before its
+  // own act (wab2_get_obs: o = [i, i + 1), nothing acts; wab2_take_action: a = [i, i + 1))
+  int32_t a0, a1, o0, o1;
+  uint32_t magic_o;       // ceil(2^20 / (o1 - o0)): q / (o1 - o0) for q < 2048
 };
 
 __device__ __forceinline__ int pymod(int a, int m) {
@@ -216,6 +220,22 @@ __device__ __forceinline__ void fetch_actions_wave(const TParams& p, int t, int6
   }
 }
 
+// reward / done of an entity after its own update (compute_reward World.py:21-22, 54-58,
+// 84-85; is_entity_done :339-343): ostrich 1 while alive (int), wolf food > 10 (bool), bush 0;
+// done: ostrich status != 0, wolf status == 1 (never set), bush always
+__device__ __forceinline__ void reward_done(int type, int status, double food_after, float& rew, uint8_t& dn) {
+  if (type == T_OSTRICH) {
+    rew = status == 0 ? 1.0f : 0.0f;
+    dn = status != 0;
+  } else if (type == T_WOLF) {
+    rew = food_after > 10.0 ? 1.0f : 0.0f;
+    dn = 0;
+  } else {
+    rew = 0.0f;
+    dn = 1;
+  }
+}
+
 template <int NMAX>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) wab_torus_kernel(TParams p0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -229,34 +249,33 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   const TParams p = kparams(p0);                                                          \
   const Lds s = lds_tables(smem, p);                                                      \
   const int N = p.N, NO = p.NO, NM = p.NM, NB = p.NB, R = p.R, W = p.W, H = p.H;          \
-  const int nent = N * kWorlds;                                                           \
-  (void)NO; (void)NM; (void)NB; (void)R; (void)W; (void)H; (void)nent
+  const int nent = N * kWorlds, a0 = p.a0, a1 = p.a1, na = a1 - a0;                       \
+  (void)NO; (void)NM; (void)NB; (void)R; (void)W; (void)H; (void)nent; (void)na
 
   // ---- prologue: state -> LDS tables, one lane per (entity, world); turn 0's actions
   {
-  WAB2_PHASE_PARAMS;
-  for (int q = tid; q < nent; q += kThreads) {
-    const int e = q >> 6, w = q & 63;
-    const int64_t a = (int64_t)e * p.Bp + wg0 + w;
-    s.pos[e * kWorlds + w] = p.df[a];
-    if (e < NM) {
-      s.oxy[e * kWorlds + w] = make_int2(p.ox[a], p.oy[a]);
-      s.food[e * kWorlds + w] = p.food[(int64_t)e * p.Bp + wg0 + w];
-    } else {
-      const int b = e - NM;
-      s.bxy[b * kWorlds + w] = (uint16_t)((p.ox[a] & 0xFF) | ((p.oy[a] & 0xFF) << 8));
-      s.bf0[b * kWorlds + w] = p.bfood[(int64_t)b * p.Bp + wg0 + w];
+    WAB2_PHASE_PARAMS;
+    for (int q = tid; q < nent; q += kThreads) {
+      const int e = q >> 6, w = q & 63;
+      const int64_t a = (int64_t)e * p.Bp + wg0 + w;
+      s.pos[e * kWorlds + w] = p.df[a];
+      if (e < NM) {
+        s.oxy[e * kWorlds + w] = make_int2(p.ox[a], p.oy[a]);
+        s.food[e * kWorlds + w] = p.food[(int64_t)e * p.Bp + wg0 + w];
+      } else {
+        const int b = e - NM;
+        s.bxy[b * kWorlds + w] = (uint16_t)((p.ox[a] & 0xFF) | ((p.oy[a] & 0xFF) << 8));
+        s.bf0[b * kWorlds + w] = p.bfood[(int64_t)b * p.Bp + wg0 + w];
+      }
+      if (e < NO) s.ost[e * kWorlds + w] = p.ost[(int64_t)e * p.Bp + wg0 + w];
+      if (e == 0) {
+        s.turn[w] = p.turn[wg0 + w];
+        s.ep[w] = p.episode[wg0 + w];
+      }
     }
-    if (e < NO) s.ost[e * kWorlds + w] = p.ost[(int64_t)e * p.Bp + wg0 + w];
-    if (e == 0) {
-      s.turn[w] = p.turn[wg0 + w];
-      s.ep[w] = p.episode[wg0 + w];
-    }
-  }
-  {
-    const int8_t* src = p.actions + wg0 * N;
-    for (int q = tid; q < nent; q += kThreads) s.act0[q] = q < nvalid * N ? (uint8_t)src[q] : (uint8_t)0;
-  }
+    // the acting entities' actions, [world][a1 - a0] as in HBM
+    const int8_t* src = p.actions + wg0 * na;
+    for (int q = tid; q < kWorlds * na; q += kThreads) s.act0[q] = q < nvalid * na ? (uint8_t)src[q] : (uint8_t)0;
   }
   __syncthreads();
 
@@ -271,13 +290,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       for (int b = 0; b < NB; ++b) s.bf1[b * kWorlds + w] = s.bf0[b * kWorlds + w];
       const uint64_t ek = world_key(p, wg0 + w, s.ep[w]);
       const int32_t turn = s.turn[w];
-      for (int k = 0; k < NO; ++k) {
-        const int a = (int)(int8_t)A[w * N + k];
+      for (int k = a0; k < min(a1, NO); ++k) {
+        const int a = (int)(int8_t)A[w * na + k - a0];
         const int2 xy = s.oxy[k * kWorlds + w];
         const uint32_t np = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
         reinterpret_cast<uint16_t*>(&s.pos[k * kWorlds + w])[1] = (uint16_t)np;
         // the visible bushes on the tile, in frame (id) order: every bush is visible (the
-        // Visible update of World.py:131 writes a copy), at its turn-start frame position
+        // Visible update of World.py:131 writes a copy), at its frame position (bushes act last)
         int n = 0;
         for (int b = 0; b < NB; ++b) n += (s.pos[(NM + b) * kWorlds + w] & 0xFFFFu) == np;
         uint32_t ev = 0xFFu, gain = 0;
@@ -307,23 +326,27 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       const int w = lane;
       const uint64_t ek = world_key(p, wg0 + w, s.ep[w]);
       const int32_t turn = s.turn[w];
-      uint32_t opos[kOMax];  // the ostriches' frame X|Y after their acts (they act first)
+      uint32_t opos[kOMax];  // the ostriches' frame X|Y (after their acts: they act first)
       uint32_t vis = 0, dead = 0, kills = 0, hid_by[kOMax];
 #pragma unroll
       for (int k = 0; k < kOMax; ++k) {
         opos[k] = 0xFFFFFFFFu;
         hid_by[k] = 0xFFu;
         if (k < NO) {
-          const int a = (int)(int8_t)A[w * N + k];
-          const int2 xy = s.oxy[k * kWorlds + w];
-          opos[k] = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
+          const uint32_t pk = s.pos[k * kWorlds + w];
+          opos[k] = pk & 0xFFFFu;
+          if (k >= a0 && k < a1) {  // acts in this launch (phase A's W0 writes the same into hi16)
+            const int a = (int)(int8_t)A[w * na + k - a0];
+            const int2 xy = s.oxy[k * kWorlds + w];
+            opos[k] = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
+          }
           const uint32_t ob = s.ost[k * kWorlds + w];
           vis |= (uint32_t)ost_visible(ob) << k;
           dead |= (uint32_t)(ost_status(ob) != 0) << k;
         }
       }
-      for (int m = NO; m < NM; ++m) {
-        const int a = (int)(int8_t)A[w * N + m];
+      for (int m = max(a0, NO); m < min(a1, NM); ++m) {
+        const int a = (int)(int8_t)A[w * na + m - a0];
         const int2 xy = s.oxy[m * kWorlds + w];
         const uint32_t np = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
         reinterpret_cast<uint16_t*>(&s.pos[m * kWorlds + w])[1] = (uint16_t)np;
@@ -356,9 +379,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           s.killed[k * kWorlds + w] = (uint8_t)(kills >> k & 1u);
         }
       dead |= kills;
-      // the batched surface's autoreset: every ostrich done, or max_turns reached
-      const bool all_dead = NO > 0 && dead == (NO >= 32 ? 0xFFFFFFFFu : (1u << NO) - 1u);
-      const bool rs = p.autoreset && (all_dead || (p.max_turns > 0 && turn + 1 >= p.max_turns));
+      // the turn ends with this launch when its last entity acts; then the batched surface's
+      // autoreset: every ostrich done, or max_turns reached
+      const bool all_dead = NO > 0 && dead == (1u << NO) - 1u;
+      const bool rs = a1 == N && p.autoreset && (all_dead || (p.max_turns > 0 && turn + 1 >= p.max_turns));
       s.ep_reset[w] = rs ? s.ep[w] + 1u : 0u;
       const bool valid = w < nvalid;
       if (p.world_reset && valid) p.world_reset[(int64_t)t * p.B + wg0 + w] = (uint8_t)rs;
@@ -367,7 +391,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       WAB2_PHASE_PARAMS;
       // bushes act on nothing (World.py:9-10); their frame X/Y become x mod W, y mod H
       const int w = lane;
-      for (int b = 0; b < NB; ++b) {
+      for (int b = max(a0, NM) - NM; b < a1 - NM; ++b) {
         const uint32_t bxy = s.bxy[b * kWorlds + w];
         const uint32_t np = (uint32_t)pymod((int)(bxy & 0xFFu), W) | ((uint32_t)pymod((int)(bxy >> 8), H) << 8);
         reinterpret_cast<uint16_t*>(&s.pos[(NM + b) * kWorlds + w])[1] = (uint16_t)np;
@@ -378,16 +402,19 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     }
     __syncthreads();
 
-    // ================= phase B: observation records, reward, done.  Rounds of 32 (world,
-    // observer) items per wave; lanes l and l + 32 share item l: each computes half of the
-    // observer's view (delta dwords k = 2kk + half, i.e. entities 4kk + 2 half + {0, 1}), so a
-    // round's 32 records fit the wave's LDS stage and every lane is busy
+    // ================= phase B: observation records (and, for a whole turn, reward and done).
+    // Rounds of 32 (world, observer) items per wave; lanes l and l + 32 share item l: each
+    // computes half of the observer's view (delta dwords k = 2kk + half, i.e. entities
+    // 4kk + 2 half + {0, 1}), so a round's 32 records fit the wave's LDS stage and every lane
+    // is busy
     {
       WAB2_PHASE_PARAMS;
-      const int nitems = nvalid * N;
+      const int o0 = p.o0, no = p.o1 - p.o0;
+      const int nitems = nvalid * no;
       uint8_t* stage = s.stage + wave * 32 * R;
-      const int64_t item0 = wg0 * N;  // first item of the workgroup in [B][N]
-      uint8_t* obs_t = p.obs + (int64_t)t * p.B * N * R;
+      const int64_t item0 = wg0 * no;  // first item of the workgroup in [B][no]
+      uint8_t* obs_t = p.obs + (int64_t)t * p.B * no * R;
+      const bool whole_turn = a0 == 0 && a1 == N && o0 == 0 && no == N;
       const int hf = lane >> 5;
       const int nd = (2 * N + 3) >> 2;  // delta dwords
       const int bb = 24 + 2 * N;        // first bush-food byte
@@ -395,8 +422,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const int q = rnd * 32 + (lane & 31);
         const bool on = q < nitems;
         const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
-        const int w = (int)(((uint32_t)qc * p.magic_n) >> 20);
-        const int i = qc - w * N;
+        const int w = (int)(((uint32_t)qc * p.magic_o) >> 20);
+        const int i = o0 + qc - w * no;
         const int type = i < NO ? T_OSTRICH : i < NM ? T_WOLF : T_BUSH;
         const uint32_t pi = s.pos[i * kWorlds + w];
         const int ex = (int)(pi & 0xFFu), ey = (int)((pi >> 8) & 0xFFu);
@@ -410,8 +437,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         // dx - W when X >= W - (r - x) and |dx - W| < |dx|; the `elif` side by dx + W
         const int lox = ex < r ? W - r : 0x7FFF, hix = (ex >= r && W < ex + r) ? r - W : -0x7FFF;
         const int loy = ey < r ? H - r : 0x7FFF, hiy = (ey >= r && H < ey + r) ? r - H : -0x7FFF;
-        // ostriches still Visible when i observes: visible at the turn start and not hidden
-        // by a wolf that acted before i
+        // ostriches still Visible when i observes: visible before the launch and not hidden
+        // by a wolf of this launch that acted before i
         uint32_t alive = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < kOMax; ++k)
@@ -420,6 +447,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const int h = s.hid[k * kWorlds + w];
             if (!ost_visible(okb) || h < i) alive &= ~(1u << k);
           }
+        // entity j is where observer i sees it: after its act if it acted in this launch
+        // before i (a0 <= j < i), else at its frame position from before the launch
+        const int jn = min(i, a1);
         uint32_t vis = 0, d[NMAX / 4];
 #pragma unroll
         for (int kk = 0; kk < NMAX / 4; ++kk) {
@@ -429,7 +459,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const int j = 4 * kk + 2 * hf + u;
             if (j < N) {
               const uint32_t pj = s.pos[j * kWorlds + w];
-              const uint32_t xy = j < i ? pj >> 16 : pj & 0xFFFFu;
+              const uint32_t xy = (j >= a0 && j < jn) ? pj >> 16 : pj & 0xFFFFu;
               int dx = (int)(xy & 0xFFu) - ex, dy = (int)(xy >> 8) - ey;
               dx = (dx >= lox && 2 * dx > W) ? dx - W : dx;
               dx = (dx <= hix && 2 * dx < -W) ? dx + W : dx;
@@ -458,21 +488,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           food = s.food[i * kWorlds + w];
         }
         const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
-        if (on && hf == 0) {
-          // reward / done after the entity's own update (compute_reward, is_entity_done)
+        if (whole_turn && on && hf == 0) {
           float rew;
           uint8_t dn;
-          if (type == T_OSTRICH) {
-            rew = status == 0 ? 1.0f : 0.0f;
-            dn = status != 0;
-          } else if (type == T_WOLF) {
-            const double fa = s.gain[i * kWorlds + w] ? food + p.wff : food;
-            rew = fa > 10.0 ? 1.0f : 0.0f;
-            dn = 0;
-          } else {
-            rew = 0.0f;
-            dn = 1;
-          }
+          reward_done(type, status, type == T_WOLF && s.gain[i * kWorlds + w] ? food + p.wff : food, rew, dn);
           p.reward[(int64_t)t * p.B * N + item0 + q] = rew;
           p.done[(int64_t)t * p.B * N + item0 + q] = dn;
         }
@@ -488,13 +507,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         for (int kk = 0; kk < NMAX / 4; ++kk)
           if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
         // Additional_Data [food] of the visible bushes as the observer sees them: after the
-        // eats of the ostriches that acted before it
+        // eats of the ostriches that acted before it in this launch
         for (int b = hf; b < NB; b += 2) {
           uint32_t f = 0;
           if (vis >> (NM + b) & 1u) {
             if (type == T_OSTRICH) {
               f = s.bf0[b * kWorlds + w];
-              for (int k = 0; k < NO; ++k)
+              for (int k = a0; k < min(a1, NO); ++k)
                 if (k < i) {
                   const uint32_t e = s.ev[k * kWorlds + w];
                   if ((e & 0xFFu) == (uint32_t)b) f = e >> 8;
@@ -522,84 +541,100 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     }
     __syncthreads();
 
-    // ================= phase C: the turn's end, one lane per (entity, world)
+    // ================= phase C: the launch's end, one lane per (entity, world): the acting
+    // entities' moves, roles and food, every ostrich's kills, the bushes' food, the autoreset
     {
-    WAB2_PHASE_PARAMS;
-    const uint8_t* A = (t & 1) ? s.act1 : s.act0;
-    for (int q = tid; q < nent; q += kThreads) {
-      const int e = q >> 6, w = q & 63;
-      const uint32_t epr = s.ep_reset[w];
-      uint32_t pe = s.pos[e * kWorlds + w];
-      s.pos[e * kWorlds + w] = pe >> 16;  // the frame X/Y after the act (a reset leaves it)
-      const int a = (int)(int8_t)A[w * N + e];
-      int nx = 0, ny = 0;
-      if (epr) {  // reset_environment: randint(0, W), randint(0, H) (WAB_Environment2_Single.py:45-46)
-        const uint64_t ek = world_key(p, wg0 + w, epr);
-        nx = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)W + 1u);
-        ny = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)H + 1u);
-      }
-      if (e < NM) {
-        int2 xy = s.oxy[e * kWorlds + w];
-        xy.x += move_dx(a);
-        xy.y += move_dy(a);
-        double f = s.food[e * kWorlds + w];
-        const uint32_t g = s.gain[e * kWorlds + w];
-        if (e < NO) {
-          f += (double)g;
-          uint32_t ob = s.ost[e * kWorlds + w];
-          if (a == 4) ob &= ~4u;
-          if (a == 5) ob |= 4u;
-          if (s.killed[e * kWorlds + w]) ob = (ob & ~3u) | 2u;
-          if (s.hid[e * kWorlds + w] != 0xFFu) ob &= ~8u;
-          if (epr) ob = ((uint32_t)p.role0 << 2) | 8u;
-          s.ost[e * kWorlds + w] = (uint8_t)ob;
-          if (epr) f = p.ofood0;
-        } else {
-          if (g) f += p.wff;
-          if (epr) f = p.wfood0;
+      WAB2_PHASE_PARAMS;
+      const uint8_t* A = (t & 1) ? s.act1 : s.act0;
+      const bool whole_turn = a0 == 0 && a1 == N && p.o0 == 0 && p.o1 == N;
+      for (int q = tid; q < nent; q += kThreads) {
+        const int e = q >> 6, w = q & 63;
+        const uint32_t epr = s.ep_reset[w];
+        const bool acts = e >= a0 && e < a1;
+        if (acts) s.pos[e * kWorlds + w] >>= 16;  // the frame X/Y after the act (a reset leaves it)
+        const int a = acts ? (int)(int8_t)A[w * na + e - a0] : -1;
+        int nx = 0, ny = 0;
+        if (epr) {  // reset_environment: randint(0, W), randint(0, H) (WAB_Environment2_Single.py:45-46)
+          const uint64_t ek = world_key(p, wg0 + w, epr);
+          nx = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)W + 1u);
+          ny = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)H + 1u);
         }
-        if (epr) xy = make_int2(nx, ny);
-        s.oxy[e * kWorlds + w] = xy;
-        s.food[e * kWorlds + w] = f;
-      } else {
-        const int b = e - NM;
-        s.bf0[b * kWorlds + w] = epr ? (uint8_t)p.fpb : s.bf1[b * kWorlds + w];
-        if (epr) s.bxy[b * kWorlds + w] = (uint16_t)(nx | (ny << 8));
+        if (e < NM) {
+          int2 xy = s.oxy[e * kWorlds + w];
+          xy.x += move_dx(a);
+          xy.y += move_dy(a);
+          double f = s.food[e * kWorlds + w];
+          const uint32_t g = acts ? s.gain[e * kWorlds + w] : 0u;
+          const uint32_t ob0 = e < NO ? s.ost[e * kWorlds + w] : 0u;  // before this launch's kills
+          if (e < NO) {
+            f += (double)g;
+            uint32_t ob = ob0;
+            if (a == 4) ob &= ~4u;
+            if (a == 5) ob |= 4u;
+            if (s.killed[e * kWorlds + w]) ob = (ob & ~3u) | 2u;
+            if (s.hid[e * kWorlds + w] != 0xFFu) ob &= ~8u;
+            if (epr) ob = ((uint32_t)p.role0 << 2) | 8u;
+            s.ost[e * kWorlds + w] = (uint8_t)ob;
+          } else {
+            if (g) f += p.wff;
+          }
+          const double f_act = f;  // after the act, before a reset at the turn's end
+          if (epr) f = e < NO ? p.ofood0 : p.wfood0;
+          if (!whole_turn && acts && w < nvalid) {
+            // take_action's (reward, done): an ostrich's status as its own update left it (the
+            // wolves that may kill it act after it), a wolf's food after its update
+            float rew;
+            uint8_t dn;
+            reward_done(e < NO ? T_OSTRICH : T_WOLF, ost_status(ob0), f_act, rew, dn);
+            p.reward[(int64_t)(wg0 + w) * na + e - a0] = rew;
+            p.done[(int64_t)(wg0 + w) * na + e - a0] = dn;
+          }
+          if (epr) xy = make_int2(nx, ny);
+          s.oxy[e * kWorlds + w] = xy;
+          s.food[e * kWorlds + w] = f;
+        } else {
+          const int b = e - NM;
+          s.bf0[b * kWorlds + w] = epr ? (uint8_t)p.fpb : s.bf1[b * kWorlds + w];
+          if (epr) s.bxy[b * kWorlds + w] = (uint16_t)(nx | (ny << 8));
+          if (!whole_turn && acts && w < nvalid) {
+            p.reward[(int64_t)(wg0 + w) * na + e - a0] = 0.0f;
+            p.done[(int64_t)(wg0 + w) * na + e - a0] = 1;
+          }
+        }
+        if (e == 0 && a1 == N && na > 0) {  // the turn ends: World.increment_turn (WAB_Environment2.py:131-133)
+          s.turn[w] = epr ? 0 : s.turn[w] + 1;
+          if (epr) s.ep[w] = epr;
+        }
       }
-      if (e == 0) {
-        s.turn[w] = epr ? 0 : s.turn[w] + 1;
-        if (epr) s.ep[w] = epr;
-      }
-    }
     }
     __syncthreads();
   }
 
   // ---- epilogue: LDS tables -> state
   {
-  WAB2_PHASE_PARAMS;
-  for (int q = tid; q < nent; q += kThreads) {
-    const int e = q >> 6, w = q & 63;
-    const int64_t a = (int64_t)e * p.Bp + wg0 + w;
-    p.df[a] = (uint16_t)s.pos[e * kWorlds + w];
-    if (e < NM) {
-      const int2 xy = s.oxy[e * kWorlds + w];
-      p.ox[a] = xy.x;
-      p.oy[a] = xy.y;
-      p.food[(int64_t)e * p.Bp + wg0 + w] = s.food[e * kWorlds + w];
-    } else {
-      const int b = e - NM;
-      const uint32_t bxy = s.bxy[b * kWorlds + w];
-      p.ox[a] = (int32_t)(bxy & 0xFFu);
-      p.oy[a] = (int32_t)(bxy >> 8);
-      p.bfood[(int64_t)b * p.Bp + wg0 + w] = s.bf0[b * kWorlds + w];
+    WAB2_PHASE_PARAMS;
+    for (int q = tid; q < nent; q += kThreads) {
+      const int e = q >> 6, w = q & 63;
+      const int64_t a = (int64_t)e * p.Bp + wg0 + w;
+      p.df[a] = (uint16_t)s.pos[e * kWorlds + w];
+      if (e < NM) {
+        const int2 xy = s.oxy[e * kWorlds + w];
+        p.ox[a] = xy.x;
+        p.oy[a] = xy.y;
+        p.food[(int64_t)e * p.Bp + wg0 + w] = s.food[e * kWorlds + w];
+      } else {
+        const int b = e - NM;
+        const uint32_t bxy = s.bxy[b * kWorlds + w];
+        p.ox[a] = (int32_t)(bxy & 0xFFu);
+        p.oy[a] = (int32_t)(bxy >> 8);
+        p.bfood[(int64_t)b * p.Bp + wg0 + w] = s.bf0[b * kWorlds + w];
+      }
+      if (e < NO) p.ost[(int64_t)e * p.Bp + wg0 + w] = s.ost[e * kWorlds + w];
+      if (e == 0) {
+        p.turn[wg0 + w] = s.turn[w];
+        p.episode[wg0 + w] = s.ep[w];
+      }
     }
-    if (e < NO) p.ost[(int64_t)e * p.Bp + wg0 + w] = s.ost[e * kWorlds + w];
-    if (e == 0) {
-      p.turn[wg0 + w] = s.turn[w];
-      p.episode[wg0 + w] = s.ep[w];
-    }
-  }
   }
   if (wave == 1) {  // resets of this workgroup (W1 decided them), one atomic per wave
     unsigned long long tot = (unsigned long long)resets;
@@ -607,7 +642,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     if (lane == 0 && tot) atomicAdd(&p0.counters[1], tot);
   }
-  if (blockIdx.x == 0 && tid == 0) atomicAdd(&p0.counters[0], (unsigned long long)p0.B * (unsigned long long)T);
+  if (blockIdx.x == 0 && tid == 0 && p0.a1 == p0.N && p0.a1 > p0.a0)
+    atomicAdd(&p0.counters[0], (unsigned long long)p0.B * (unsigned long long)T);
 #undef WAB2_PHASE_PARAMS
 }
 
@@ -659,6 +695,7 @@ using wab2::TParams;
 
 struct wab2_handle {
   TParams p;
+  int next_entity = 0;  // the entity whose take_action comes next this turn (the same in every world)
   int device = 0;
   int n_blocks = 0;
   size_t lds = 0;
@@ -757,7 +794,9 @@ int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t wo
   p.role0 = cfg->starting_role;
   p.max_turns = cfg->max_turns;
   p.autoreset = cfg->autoreset ? 1 : 0;
-  p.magic_n = (uint32_t)(((1u << 20) + (uint32_t)p.N - 1u) / (uint32_t)p.N);
+  p.a0 = p.o0 = 0;
+  p.a1 = p.o1 = p.N;
+  p.magic_o = (uint32_t)(((1u << 20) + (uint32_t)p.N - 1u) / (uint32_t)p.N);
   p.B = batch;
   h->n_blocks = (int)((batch + wab2::kWorlds - 1) / wab2::kWorlds);
   p.Bp = (int64_t)h->n_blocks * wab2::kWorlds;
@@ -815,6 +854,10 @@ int64_t wab2_batch(const wab2_handle* h) { return h ? h->p.B : 0; }
 
 int wab2_reset(wab2_handle* h, const uint8_t* mask, void* stream) {
   if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
+  if (mask && h->next_entity != 0)
+    return fail(WAB2_E_INVALID, "wab2_reset: a masked reset only between turns (entity " +
+                                    std::to_string(h->next_entity) + " acts next)");
+  h->next_entity = 0;  // reset_environment: num_entities_acted_this_turn = 0 (WAB_Environment2.py:117)
   DeviceGuard2 dg(h->device);
   TParams p = h->p;
   p.mask = mask;
@@ -830,6 +873,9 @@ int wab2_rollout(wab2_handle* h, const int8_t* actions, int32_t T, uint8_t* obs,
   if (T < 1) return fail(WAB2_E_INVALID, "T must be >= 1");
   if (!actions || !obs || !reward || !done) return fail(WAB2_E_INVALID, "actions, obs, reward and done are required");
   if (reinterpret_cast<uintptr_t>(obs) & 15u) return fail(WAB2_E_INVALID, "obs must be 16-byte aligned");
+  if (h->next_entity != 0)
+    return fail(WAB2_E_INVALID, "wab2_step/wab2_rollout: a turn is half done (entity " +
+                                    std::to_string(h->next_entity) + " acts next: wab2_take_action)");
   DeviceGuard2 dg(h->device);
   TParams p = h->p;
   p.T = T;
@@ -848,6 +894,56 @@ int wab2_rollout(wab2_handle* h, const int8_t* actions, int32_t T, uint8_t* obs,
 int wab2_step(wab2_handle* h, const int8_t* actions, uint8_t* obs, float* reward, uint8_t* done,
               uint8_t* world_reset, void* stream) {
   return wab2_rollout(h, actions, 1, obs, reward, done, world_reset, stream);
+}
+
+int wab2_get_obs(wab2_handle* h, int32_t entity, uint8_t* obs, void* stream) {
+  if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
+  if (!obs || (reinterpret_cast<uintptr_t>(obs) & 15u)) return fail(WAB2_E_INVALID, "obs must be 16-byte aligned");
+  if (entity < h->next_entity || entity >= h->p.N)
+    return fail(WAB2_E_INVALID, "wab2_get_obs: entity " + std::to_string(entity) +
+                                    " has acted this turn or does not exist (World.get_observations asserts "
+                                    "the entity has not acted, World.py:362)");
+  DeviceGuard2 dg(h->device);
+  TParams p = h->p;
+  p.T = 1;
+  p.a0 = p.a1 = entity;  // nothing acts
+  p.o0 = entity;
+  p.o1 = entity + 1;
+  p.magic_o = 1u << 20;
+  p.obs = obs;
+  p.actions = nullptr;
+  p.reward = nullptr;
+  p.done = nullptr;
+  p.world_reset = nullptr;
+  hipLaunchKernelGGL(wab2::wab_torus_kernel<wab2::kNMax>, dim3((unsigned)h->n_blocks), dim3(wab2::kThreads), h->lds,
+                     (hipStream_t)stream, p);
+  HIP_TRY2(hipGetLastError());
+  return WAB2_OK;
+}
+
+int wab2_take_action(wab2_handle* h, int32_t entity, const int8_t* actions, float* reward, uint8_t* done,
+                     uint8_t* world_reset, void* stream) {
+  if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
+  if (!actions || !reward || !done) return fail(WAB2_E_INVALID, "actions, reward and done are required");
+  if (entity != h->next_entity)
+    return fail(WAB2_E_INVALID, "wab2_take_action: entity " + std::to_string(h->next_entity) +
+                                    " acts next (entities act in id order, once per turn)");
+  DeviceGuard2 dg(h->device);
+  TParams p = h->p;
+  p.T = 1;
+  p.a0 = entity;
+  p.a1 = entity + 1;
+  p.o0 = p.o1 = 0;  // no records
+  p.obs = nullptr;
+  p.actions = actions;
+  p.reward = reward;
+  p.done = done;
+  p.world_reset = world_reset;
+  hipLaunchKernelGGL(wab2::wab_torus_kernel<wab2::kNMax>, dim3((unsigned)h->n_blocks), dim3(wab2::kThreads), h->lds,
+                     (hipStream_t)stream, p);
+  HIP_TRY2(hipGetLastError());
+  h->next_entity = (entity + 1) % h->p.N;
+  return WAB2_OK;
 }
 
 int wab2_get_state(wab2_handle* h, int32_t* df_xy, int32_t* obj_xy, double* food, uint8_t* visible, uint8_t* status,

@@ -11,7 +11,10 @@ wab_gym_amd/csrc/wab_torus.hip (C-ABI include/wab_torus.h):
     env.reset_environment()
     obs, reward, done, info = env.step(actions)    # actions [B, N] int8: one turn of every
                                                    # world, entities in id order
-    env.get_obs(world, entity, obs)                # the reference's get_obs() result, decoded
+    env.frame(obs[b, i])                           # the reference's get_obs() result, decoded
+    # or the reference's own per-entity loop (Env2Tests.py:40-88), every world at once:
+    rec = env.get_obs(i)                           # [B, R]
+    reward, done, info = env.take_action(i, a)     # a [B]
 
 `obs` is [B, N, R] uint8 records (include/wab_torus.h): record [b, i] is what entity i's
 `get_obs()` returned in world b at its place in the turn (after entities < i acted), i.e. the
@@ -140,6 +143,30 @@ class BatchedWABEnvironment2:
                                              done.data_ptr(), wr.data_ptr(), self._stream()), "wab2_rollout")
         return obs, rew, done, wr
 
+    def get_obs(self, entity_id):
+        """WAB_Environment2.get_obs(entity_id) (:120-123) in every world: records [B, R] u8 of
+        that entity as it is now (decode one with `frame`).  Any entity that has not acted in
+        the current turn."""
+        obs = self._torch.empty((self.num_worlds, self.R), dtype=self._torch.uint8, device=self.device)
+        _lib.check2(_lib.load().wab2_get_obs(self._h, int(entity_id), obs.data_ptr(), self._stream()),
+                    "wab2_get_obs")
+        return obs
+
+    def take_action(self, entity_id, actions):
+        """WAB_Environment2.take_action(entity_id, action) (:125-134) in every world: actions [B]
+        -> (reward [B] f32, done [B] bool, {"world_reset": [B] bool}).  Entities act in id
+        order, each once per turn; the call of the last entity ends the turn (and, with
+        autoreset, resets the worlds that are over)."""
+        t = self._torch
+        a = self._actions(actions, (self.num_worlds,))
+        rew = t.empty(self.num_worlds, dtype=t.float32, device=self.device)
+        done = t.empty(self.num_worlds, dtype=t.uint8, device=self.device)
+        wr = t.empty(self.num_worlds, dtype=t.uint8, device=self.device)
+        _lib.check2(_lib.load().wab2_take_action(self._h, int(entity_id), a.data_ptr(), rew.data_ptr(),
+                                                 done.data_ptr(), wr.data_ptr(), self._stream()),
+                    "wab2_take_action")
+        return rew, done.bool(), {"world_reset": wr.bool()}
+
     # ------------------------------------------------------------------ decoding
     def fields(self, obs):
         """Typed views of records [..., N, R]: food f64, x/y i32, visible u32 (bit j: entity j
@@ -157,13 +184,13 @@ class BatchedWABEnvironment2:
         del R
         return f
 
-    def get_obs(self, world, entity, obs=None):
-        """The reference's get_obs(entity) (World.get_observations, World.py:360-377) of one
-        world, decoded from a record: [rows, internal obs] with rows = [(index, Delta_X, Delta_Y,
-        Type, Additional_Data)] in id order (the visible-objects frame after reset_index) and
-        internal = [x, y, food, role, status] (ostrich), [x, y, food, is_running, status]
-        (wolf) or [x, y, food] (bush)."""
-        rec = (self.obs if obs is None else obs)[world, entity].cpu().numpy()
+    def frame(self, record):
+        """One record (a [R] u8 tensor or array, e.g. obs[b, i] of step() or get_obs(i)[b])
+        decoded into the reference's get_obs() result (World.get_observations, World.py:360-377):
+        [rows, internal obs], rows = [(index, Delta_X, Delta_Y, Type, Additional_Data)] in id
+        order (the visible-objects frame after reset_index), internal = [x, y, food, role,
+        status] (ostrich), [x, y, food, is_running, status] (wolf) or [x, y, food] (bush)."""
+        rec = record.cpu().numpy() if hasattr(record, "cpu") else record
         return decode_record(rec, self.types, self.num_bushes)
 
     def state(self):
