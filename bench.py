@@ -400,20 +400,28 @@ def run_torus(args, dev, rank, world):
     env.reset_environment()
     run(0, W, stream)
     torch.cuda.synchronize(dev)
-    graph = torch.cuda.CUDAGraph()
-    side = torch.cuda.Stream(dev)
-    side.wait_stream(stream)
-    with torch.cuda.stream(side):
-        with torch.cuda.graph(graph, stream=side):
-            run(W, K, torch.cuda.current_stream(dev))
-    stream.wait_stream(side)
-    torch.cuda.synchronize(dev)
-    env.reset_environment()  # the capture did not execute the turns: rewind
-    run(0, W, stream)
-    torch.cuda.synchronize(dev)
+    graph = None
+    if args.mode == "graph":
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(graph, stream=side):
+                run(W, K, torch.cuda.current_stream(dev))
+        stream.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        env.reset_environment()  # the capture did not execute the turns: rewind
+        run(0, W, stream)
+        torch.cuda.synchronize(dev)
+
+    def replay_once():
+        if graph is not None:
+            graph.replay()
+        else:
+            run(W, K, stream)
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     c0.record(stream)
-    graph.replay()
+    replay_once()
     c1.record(stream)
     torch.cuda.synchronize(dev)
     reps = window_replays(c0.elapsed_time(c1) * 1e-3)
@@ -427,7 +435,7 @@ def run_torus(args, dev, rank, world):
     t_wall = time.perf_counter()
     ev0.record(stream)
     for _ in range(reps):
-        graph.replay()
+        replay_once()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t_wall
@@ -441,14 +449,16 @@ def run_torus(args, dev, rank, world):
     alg = torus_alg_bytes(NO, NW, NB, T)
     # the per-step surface beside it: one wab2_step launch per turn, records into a 32-slot ring
     NR = 32
-    ring = torch.empty((NR, B, N, R), dtype=torch.uint8, device=dev)
-    ring_rd = torch.empty((NR, B, N), dtype=torch.float32, device=dev)
-    ring_dn = torch.empty((NR, B, N), dtype=torch.uint8, device=dev)
-    ps_ms, ps_n = time_launches(
-        lambda i, s: _lib.check2(L.wab2_step(h, a0 + (W + i) * B * N, ring[i % NR].data_ptr(),
-                                             ring_rd[i % NR].data_ptr(), ring_dn[i % NR].data_ptr(), None, s),
-                                 "wab2_step"), min(K, 256), dev, stream, args.mode)
-    del ring
+    ps_ms = float("nan")
+    if not args.no_diag:
+        ring = torch.empty((NR, B, N, R), dtype=torch.uint8, device=dev)
+        ring_rd = torch.empty((NR, B, N), dtype=torch.float32, device=dev)
+        ring_dn = torch.empty((NR, B, N), dtype=torch.uint8, device=dev)
+        ps_ms, ps_n = time_launches(
+            lambda i, s: _lib.check2(L.wab2_step(h, a0 + (W + i) * B * N, ring[i % NR].data_ptr(),
+                                                 ring_rd[i % NR].data_ptr(), ring_dn[i % NR].data_ptr(), None, s),
+                                     "wab2_step"), min(K, 256), dev, stream, args.mode)
+        del ring
     ps_alg = torus_alg_bytes(NO, NW, NB, 1)
     achieved = alg * B / (kern_ms * 1e-3) / 1e9
     per_rank = all_gather_objects({"rank": rank, "device": str(dev), "pci": pci_id(dev),

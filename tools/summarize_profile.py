@@ -46,19 +46,21 @@ def main(src, dst, kernel=r"wab_kernel<0|wab_step_q4"):
     m = summ["pmc_mean_per_dispatch"]
     if "SQ_ACTIVE_INST_VALU" in m and "SQ_WAVES" in m:
         # SQ_ACTIVE_INST_VALU tracks SQ_INSTS_VALU one for one on this kernel shape, so it is
-        # taken as instructions, each holding its SIMD 4 cycles (a wave64 on 16 lanes; simple
-        # ops issue faster, tools/micro/valu_rate.hip: ~2.5 cycles, multiplies ~4.4).  The
-        # launch's cycles are its rocprofv3 duration at the nominal 2.4 GHz: GRBM_GUI_ACTIVE / 8
-        # reads high on dispatches this short (MI355X_MICROARCH.md, DVFS give-back).
+        # taken as instructions.  A SIMD-32 issues one wave64 VALU instruction per 2 cycles when
+        # two or more waves feed it (MI355X_MICROARCH.md: v_fma_f32 2 cyc; 4 for one wave
+        # alone), so the pipe's busy fraction counts 2 cycles per instruction (rounds 1-4 of
+        # this repo counted 4, twice the pipe's occupancy).  The launch's cycles are its
+        # rocprofv3 duration at the nominal 2.4 GHz: GRBM_GUI_ACTIVE / 8 reads high on
+        # dispatches this short (MI355X_MICROARCH.md, DVFS give-back).
         simds = 256 * 4
         v = {"insts_per_wave": m["SQ_INSTS_VALU"] / m["SQ_WAVES"],
              "salu_insts_per_wave": m.get("SQ_INSTS_SALU", 0.0) / m["SQ_WAVES"],
-             "issue_cycles_per_simd": 4.0 * m["SQ_ACTIVE_INST_VALU"] / simds}
+             "issue_cycles_per_simd": 2.0 * m["SQ_ACTIVE_INST_VALU"] / simds}
         if "trace" in summ:
             cyc = summ["trace"]["avg_ns"] * 2.4
             v["launch_cycles_at_2.4GHz"] = cyc
             v["busy_frac"] = v["issue_cycles_per_simd"] / cyc
-        v["source"] = ("SQ_INSTS_VALU / SQ_WAVES; busy = 4 cycles * SQ_ACTIVE_INST_VALU / 1024 SIMDs / "
+        v["source"] = ("SQ_INSTS_VALU / SQ_WAVES; busy = 2 cycles * SQ_ACTIVE_INST_VALU / 1024 SIMDs / "
                        "(rocprofv3 avg duration * 2.4 GHz)")
         summ["valu"] = v
     json.dump(summ, open(os.path.join(dst, "summary.json"), "w"), indent=1)
