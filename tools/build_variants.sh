@@ -8,11 +8,11 @@ O=/tmp/wab_variants
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Werror"
 mkdir -p $O $REPO/wab_gym_amd/_lib/var
 VAR=${VARIANT_SRC:-wab_step_small}   # the source compiled per variant; the others once
-ALL="wab_step wab_step_small wab_step_wide wab_features wab_render wab_egocentric wab_capi"
+ALL="wab_step wab_step_small wab_step_wide wab_features wab_render wab_egocentric wab_torus wab_capi"
 COMMON=$(for x in $ALL; do [ $x = $VAR ] || echo $x; done)
 for x in $COMMON; do
   fresh=1
-  for d in $C/$x.hip $C/*.h $REPO/include/wab.h; do [ $O/$x.o -nt $d ] || fresh=0; done
+  for d in $C/$x.hip $C/*.h $REPO/include/wab.h $REPO/include/wab_torus.h; do [ $O/$x.o -nt $d ] || fresh=0; done
   [ $fresh = 1 ] || /opt/rocm/bin/hipcc $F -c $C/$x.hip -o $O/$x.o &
 done
 wait

@@ -39,7 +39,7 @@ for s in "$@"; do
       cat "$out/stamps_${arg//[ ,-]/_}.log" ;;
     prof)
       cfg=${arg:-default}
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_$cfg" -o run -- python3 bench.py --config "$cfg" --no-cpu > "$out/prof_$cfg.log" 2>&1 || { tail -30 "$out/prof_$cfg.log"; exit 1; }
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_$cfg" -o run -- python3 bench.py --config "$cfg" --no-cpu > "$out/prof_$cfg.log" 2>&1 || { tail -30 "$out/prof_$cfg.log"; exit 1; }
       find "$out/prof_$cfg" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$out/prof_$cfg/kernel_stats.csv"
       head -5 "$out/prof_$cfg/kernel_stats.csv" ;;
     smoke)

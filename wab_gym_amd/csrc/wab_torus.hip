@@ -33,6 +33,13 @@
 #include "../../include/wab_torus.h"
 #include "wab_device.h"
 
+// Diagnostic builds only (tools/ab_torus.sh; results wrong by design): WAB2_ABLATE bit 1 skips
+// the view computation of the records, bit 2 their global stores, bit 4 the bush-food bytes,
+// bit 8 phase C.
+#ifndef WAB2_ABLATE
+#define WAB2_ABLATE 0
+#endif
+
 namespace wab2 {
 
 using wab::draw_U;
@@ -457,7 +464,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const int j = 4 * kk + 2 * hf + u;
-            if (j < N) {
+            if (j < N && !(WAB2_ABLATE & 1)) {
               const uint32_t pj = s.pos[j * kWorlds + w];
               const uint32_t xy = (j >= a0 && j < jn) ? pj >> 16 : pj & 0xFFFFu;
               int dx = (int)(xy & 0xFFu) - ex, dy = (int)(xy >> 8) - ey;
@@ -508,7 +515,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
         // Additional_Data [food] of the visible bushes as the observer sees them: after the
         // eats of the ostriches that acted before it in this launch
-        for (int b = hf; b < NB; b += 2) {
+        for (int b = hf; b < ((WAB2_ABLATE & 4) ? 0 : NB); b += 2) {
           uint32_t f = 0;
           if (vis >> (NM + b) & 1u) {
             if (type == T_OSTRICH) {
@@ -532,7 +539,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const int cnt = min(32, nitems - q0);
         const int chunks = cnt * R / 16;
         uint8_t* dst = obs_t + (item0 + q0) * (int64_t)R;
-        for (int c = lane; c < chunks; c += 64) {
+        for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
           const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16 * c);
           __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + 16 * c));
         }
@@ -547,7 +554,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       WAB2_PHASE_PARAMS;
       const uint8_t* A = (t & 1) ? s.act1 : s.act0;
       const bool whole_turn = a0 == 0 && a1 == N && p.o0 == 0 && p.o1 == N;
-      for (int q = tid; q < nent; q += kThreads) {
+      for (int q = tid; q < ((WAB2_ABLATE & 8) ? 0 : nent); q += kThreads) {
         const int e = q >> 6, w = q & 63;
         const uint32_t epr = s.ep_reset[w];
         const bool acts = e >= a0 && e < a1;
