@@ -52,7 +52,6 @@ enum : uint32_t { SITE_T_CREATE = 7, SITE_T_RESET = 8, SITE_T_EAT = 9, SITE_T_KI
 enum { T_OSTRICH = 0, T_WOLF = 1, T_BUSH = 2 };
 constexpr int kWorlds = 64;   // worlds per workgroup
 constexpr int kThreads = 256;
-constexpr int kNMax = WAB2_MAX_ENTITIES;
 constexpr int kOMax = WAB2_MAX_OSTRICHES;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -109,31 +108,41 @@ __device__ __forceinline__ int keyed_below(uint64_t ek, uint32_t site, int32_t t
 __device__ __forceinline__ int move_dx(int a) { return (a == 1) - (a == 3); }
 __device__ __forceinline__ int move_dy(int a) { return (a == 0) - (a == 2); }
 
-// LDS tables of the workgroup's 64 worlds (byte offsets from the dynamic LDS base)
+// LDS tables of the workgroup's 64 worlds.  Tables a lane-per-world phase walks by entity are
+// entity-major ([e][64]: a wave's 64 lanes read 64 consecutive words); the two that phase B reads
+// per observer are world-major, so an item reads two entities' positions with one ds_read_b64
+// and a pair of bush foods with one ds_read_u16.
 struct Lds {
-  double* food;      // [NM][64] turn start
-  int2* oxy;         // [NM][64] movers' own x, y (turn start)
+  double* food;      // [NM][64] ostrich / wolf food before the launch
+  int2* oxy;         // [NM][64] movers' own x, y (unbounded) before the launch
   uint8_t* stage;    // [4][32][R] record stage, per wave
-  uint8_t* act0;     // [64][N] raw actions (world-major, as in HBM) of even turns
+  uint8_t* act0;     // [64][na] raw actions (world-major, as in HBM) of even turns
   uint8_t* act1;     // ... of odd turns
-  uint32_t* pos;     // [N][64] lo16: frame X|Y<<8 at turn start; hi16: after the entity's act
+  uint32_t* pos;     // [64][Np] lo16: frame X|Y<<8 before the launch's acts; hi16: after the act
   int32_t* turn;     // [64]
   uint32_t* ep;      // [64]
   uint32_t* ep_reset;  // [64] episode of this turn's reset draws, 0: no reset
-  uint16_t* bxy;     // [NB][64] bushes' own x | y << 8
-  uint16_t* ev;      // [NO][64] eat of ostrich k this turn: bush index | food after << 8 (0xFF: none)
+  uint16_t* omod;    // [NM][64] movers' x mod W | y mod H << 8 (the frame X/Y their next act gives)
+  uint16_t* bxy;     // [NB][64] bushes' own x | y << 8 (in [0, W] x [0, H])
+  uint16_t* ev;      // [NO][64] eat of ostrich k in this launch: bush index | food after << 8 (0xFF: none)
+  uint8_t* bf0;      // [64][NBp] bush food before the launch's eats
+  uint8_t* bf1;      // [64][NBp] after them
   uint8_t* gain;     // [NM][64] ostrich: berries eaten; wolf: 1 if it ate an ostrich
-  uint8_t* bf0;      // [NB][64] bush food at turn start
-  uint8_t* bf1;      // [NB][64] after the ostriches' eats
-  uint8_t* ost;      // [NO][64] ostrich state byte at turn start
-  uint8_t* hid;      // [NO][64] the wolf whose kill hid label k this turn (0xFF: none)
-  uint8_t* killed;   // [NO][64] status set to 2 this turn
+  uint8_t* ost;      // [NO][64] ostrich state byte before the launch
+  uint8_t* hid;      // [NO][64] the wolf whose kill hid label k in this launch (0xFF: none)
+  uint8_t* killed;   // [NO][64] status set to 2 in this launch
 };
 
 __host__ __device__ inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 
+// position-table row: 4 entities per dword-pair group (ceil(N / 4) groups) + 2 (an even row
+// that spreads consecutive worlds over the LDS banks)
+__host__ __device__ inline int pos_row(int N) { return 4 * ((N + 3) / 4) + 2; }
+__host__ __device__ inline int bush_row(int NB) { return (NB + 3) & ~3; }
+
 struct LdsLayout {
-  size_t food, oxy, stage, act0, act1, pos, turn, ep, ep_reset, bxy, ev, gain, bf0, bf1, ost, hid, killed, total;
+  size_t food, oxy, stage, act0, act1, pos, turn, ep, ep_reset, omod, bxy, ev, bf0, bf1, gain, ost, hid, killed,
+      total;
 };
 
 __host__ __device__ inline LdsLayout lds_layout(int N, int NO, int NM, int NB, int R) {
@@ -144,15 +153,16 @@ __host__ __device__ inline LdsLayout lds_layout(int N, int NO, int NM, int NB, i
   L.stage = o; o += (size_t)4 * 32 * R;
   L.act0 = o; o += align16((size_t)kWorlds * N);
   L.act1 = o; o += align16((size_t)kWorlds * N);
-  L.pos = o; o += (size_t)N * kWorlds * 4;
+  L.pos = o; o += align16((size_t)kWorlds * pos_row(N) * 4);
   L.turn = o; o += kWorlds * 4;
   L.ep = o; o += kWorlds * 4;
   L.ep_reset = o; o += kWorlds * 4;
+  L.omod = o; o += align16((size_t)NM * kWorlds * 2);
   L.bxy = o; o += align16((size_t)NB * kWorlds * 2);
   L.ev = o; o += align16((size_t)NO * kWorlds * 2);
+  L.bf0 = o; o += align16((size_t)kWorlds * bush_row(NB));
+  L.bf1 = o; o += align16((size_t)kWorlds * bush_row(NB));
   L.gain = o; o += align16((size_t)NM * kWorlds);
-  L.bf0 = o; o += align16((size_t)NB * kWorlds);
-  L.bf1 = o; o += align16((size_t)NB * kWorlds);
   L.ost = o; o += align16((size_t)NO * kWorlds);
   L.hid = o; o += align16((size_t)NO * kWorlds);
   L.killed = o; o += align16((size_t)NO * kWorlds);
@@ -172,11 +182,12 @@ __device__ __forceinline__ Lds lds_tables(uint8_t* base, const TParams& p) {
   s.turn = reinterpret_cast<int32_t*>(base + L.turn);
   s.ep = reinterpret_cast<uint32_t*>(base + L.ep);
   s.ep_reset = reinterpret_cast<uint32_t*>(base + L.ep_reset);
+  s.omod = reinterpret_cast<uint16_t*>(base + L.omod);
   s.bxy = reinterpret_cast<uint16_t*>(base + L.bxy);
   s.ev = reinterpret_cast<uint16_t*>(base + L.ev);
-  s.gain = base + L.gain;
   s.bf0 = base + L.bf0;
   s.bf1 = base + L.bf1;
+  s.gain = base + L.gain;
   s.ost = base + L.ost;
   s.hid = base + L.hid;
   s.killed = base + L.killed;
@@ -185,6 +196,14 @@ __device__ __forceinline__ Lds lds_tables(uint8_t* base, const TParams& p) {
 
 __device__ __forceinline__ uint64_t world_key(const TParams& p, int64_t g, uint32_t ep) {
   return episode_key(p.seed, (uint64_t)(p.world_base + g), ep);
+}
+
+// v + d wrapped into [0, m), for v in [0, m) and |d| <= 1 (or v in [0, m] and d = 0)
+__device__ __forceinline__ int wrap1(int v, int m) { return v < 0 ? v + m : v >= m ? v - m : v; }
+
+// the frame X|Y<<8 an act gives a mover whose x mod W | y mod H << 8 is `om`
+__device__ __forceinline__ uint32_t moved(uint32_t om, int a, int W, int H) {
+  return (uint32_t)wrap1((int)(om & 0xFFu) + move_dx(a), W) | ((uint32_t)wrap1((int)(om >> 8) + move_dy(a), H) << 8);
 }
 
 // A fresh copy of the kernel parameters, loaded from the kernel-argument segment behind an
@@ -243,7 +262,66 @@ __device__ __forceinline__ void reward_done(int type, int status, double food_af
   }
 }
 
-template <int NMAX>
+// One observer's view of one entity j (World._get_visible_objects, World.py:243-316): the
+// (Delta_X, Delta_Y) byte pair if j is a row of the frame, else 0.  `xy` is j's frame X|Y<<8 as
+// the observer sees it.  The wrap (:255-291) is folded into thresholds on X: the `if` side
+// (x < r) replaces dx by dx - W exactly when X >= xl = max(W - r + x, x + W/2 + 1) (the
+// mask and min(key=abs) choosing the wrapped, strictly shorter delta), the `elif` side by
+// dx + W when X <= xr = min(r - W + x, x - W/2 - 1); the other side's threshold never holds.
+struct View {
+  int ex, ey, xl, xr, yl, yr, W, H, r2;
+  uint32_t alive;
+};
+
+// branch-free (bit operations, not && / ?:, so that the compiler keeps one straight line and
+// the item's position loads go out back to back): `valid` 1 for an entity that exists
+__device__ __forceinline__ uint32_t view_pair(const View& v, uint32_t xy, int j, uint32_t valid, uint32_t& vis) {
+  const int X = (int)(xy & 0xFFu), Y = (int)(xy >> 8);
+  const int dx = X - v.ex - (v.W & -(int)(X >= v.xl)) + (v.W & -(int)(X <= v.xr));
+  const int dy = Y - v.ey - (v.H & -(int)(Y >= v.yl)) + (v.H & -(int)(Y <= v.yr));
+  const uint32_t ok = valid & (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy) <= v.r2) & (v.alive >> j);
+  vis |= (ok & 1u) << j;
+  return (((uint32_t)dx & 0xFFu) | (((uint32_t)dy & 0xFFu) << 8)) & (0u - (ok & 1u));
+}
+
+// The same on packed 16-bit halves (X, Y): one v_pk op per step for both axes, the squared
+// distance one v_dot2 (the wrap thresholds as above, "never" = +/-0x4000 so that no
+// difference leaves int16)
+#ifndef WAB2_PACKED
+#define WAB2_PACKED 1
+#endif
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+struct View2 {
+  s16x2 e, lo, hi, wh;
+  int r2;
+};
+
+// the byte pair X | Y << 8 as 16-bit halves (X, Y)
+__device__ __forceinline__ s16x2 unpack_xy(uint32_t xy) {
+  return __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, xy, 0x0c010c00u));
+}
+
+// per-half sign mask of a packed difference (-1 where negative), kept as one v_pk_ashrrev_i16
+// (the compiler otherwise splits `x >> 15` of a short2 into per-half compares and selects)
+__device__ __forceinline__ s16x2 sign_mask2(s16x2 x) {
+  uint32_t r, v = __builtin_bit_cast(uint32_t, x);
+  asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(r) : "v"(v));
+  return __builtin_bit_cast(s16x2, r);
+}
+
+// raw (before the alive / exists mask) visibility bit and delta byte pair of one entity
+__device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint32_t& ok) {
+  const s16x2 P = unpack_xy(xy);
+  const s16x2 nl = sign_mask2(P - v.lo);  // -1: P < lo (no wrap down)
+  const s16x2 nr = sign_mask2(v.hi - P);  // -1: P > hi (no wrap up)
+  const s16x2 d = P - v.e - (v.wh & ~nl) + (v.wh & ~nr);
+  ok = (uint32_t)(__builtin_amdgcn_sdot2(d, d, 0, false) <= v.r2);
+  const uint32_t pair = __builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, d), 0x0c0c0200u);
+  return pair & (0u - ok);
+}
+
+template <int NKK>  // ceil(N / 4): dword-pair groups of the delta array
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) wab_torus_kernel(TParams p0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x;
@@ -257,7 +335,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   const Lds s = lds_tables(smem, p);                                                      \
   const int N = p.N, NO = p.NO, NM = p.NM, NB = p.NB, R = p.R, W = p.W, H = p.H;          \
   const int nent = N * kWorlds, a0 = p.a0, a1 = p.a1, na = a1 - a0;                       \
-  (void)NO; (void)NM; (void)NB; (void)R; (void)W; (void)H; (void)nent; (void)na
+  const int Np = pos_row(N), NBp = bush_row(NB);                                          \
+  (void)NO; (void)NM; (void)NB; (void)R; (void)W; (void)H; (void)nent; (void)na; (void)Np; (void)NBp
 
   // ---- prologue: state -> LDS tables, one lane per (entity, world); turn 0's actions
   {
@@ -265,14 +344,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     for (int q = tid; q < nent; q += kThreads) {
       const int e = q >> 6, w = q & 63;
       const int64_t a = (int64_t)e * p.Bp + wg0 + w;
-      s.pos[e * kWorlds + w] = p.df[a];
+      s.pos[w * Np + e] = p.df[a];
+      const int ox = p.ox[a], oy = p.oy[a];
       if (e < NM) {
-        s.oxy[e * kWorlds + w] = make_int2(p.ox[a], p.oy[a]);
+        s.oxy[e * kWorlds + w] = make_int2(ox, oy);
+        s.omod[e * kWorlds + w] = (uint16_t)(pymod(ox, W) | (pymod(oy, H) << 8));
         s.food[e * kWorlds + w] = p.food[(int64_t)e * p.Bp + wg0 + w];
       } else {
         const int b = e - NM;
-        s.bxy[b * kWorlds + w] = (uint16_t)((p.ox[a] & 0xFF) | ((p.oy[a] & 0xFF) << 8));
-        s.bf0[b * kWorlds + w] = p.bfood[(int64_t)b * p.Bp + wg0 + w];
+        s.bxy[b * kWorlds + w] = (uint16_t)((ox & 0xFF) | ((oy & 0xFF) << 8));
+        s.bf0[w * NBp + b] = p.bfood[(int64_t)b * p.Bp + wg0 + w];
       }
       if (e < NO) s.ost[e * kWorlds + w] = p.ost[(int64_t)e * p.Bp + wg0 + w];
       if (e == 0) {
@@ -294,32 +375,32 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       const uint8_t* A = (t & 1) ? s.act1 : s.act0;
       // ostriches in id order: act (World.py:25-43), X = x mod W (:331-332), eat (:118-132)
       const int w = lane;
-      for (int b = 0; b < NB; ++b) s.bf1[b * kWorlds + w] = s.bf0[b * kWorlds + w];
+      uint32_t* posw = s.pos + w * Np;
+      for (int k = 0; k < NBp; k += 4)
+        *reinterpret_cast<uint32_t*>(s.bf1 + w * NBp + k) = *reinterpret_cast<const uint32_t*>(s.bf0 + w * NBp + k);
       const uint64_t ek = world_key(p, wg0 + w, s.ep[w]);
       const int32_t turn = s.turn[w];
       for (int k = a0; k < min(a1, NO); ++k) {
-        const int a = (int)(int8_t)A[w * na + k - a0];
-        const int2 xy = s.oxy[k * kWorlds + w];
-        const uint32_t np = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
-        reinterpret_cast<uint16_t*>(&s.pos[k * kWorlds + w])[1] = (uint16_t)np;
+        const uint32_t np = moved(s.omod[k * kWorlds + w], (int)(int8_t)A[w * na + k - a0], W, H);
+        reinterpret_cast<uint16_t*>(posw + k)[1] = (uint16_t)np;
         // the visible bushes on the tile, in frame (id) order: every bush is visible (the
         // Visible update of World.py:131 writes a copy), at its frame position (bushes act last)
         int n = 0;
-        for (int b = 0; b < NB; ++b) n += (s.pos[(NM + b) * kWorlds + w] & 0xFFFFu) == np;
+        for (int b = 0; b < NB; ++b) n += (posw[NM + b] & 0xFFFFu) == np;
         uint32_t ev = 0xFFu, gain = 0;
         if (n > 0) {
           int j = keyed_below(ek, SITE_T_EAT, turn, k, 0, (uint32_t)n);
           int pick = 0;
           for (int b = 0; b < NB; ++b)
-            if ((s.pos[(NM + b) * kWorlds + w] & 0xFFFFu) == np) {
+            if ((posw[NM + b] & 0xFFFFu) == np) {
               if (j == 0) pick = b;
               --j;
             }
           // Bush.take_food (Bush.py:31-39)
-          int f = s.bf1[pick * kWorlds + w];
+          int f = s.bf1[w * NBp + pick];
           const int amt = f >= p.fg ? p.fg : f;
           f = f >= p.fg ? f - p.fg : 0;
-          s.bf1[pick * kWorlds + w] = (uint8_t)f;
+          s.bf1[w * NBp + pick] = (uint8_t)f;
           ev = (uint32_t)pick | ((uint32_t)f << 8);
           gain = (uint32_t)amt;
         }
@@ -331,6 +412,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       const uint8_t* A = (t & 1) ? s.act1 : s.act0;
       // wolves in id order: act (World.py:61-73), X = x mod W, kill (:107-116)
       const int w = lane;
+      uint32_t* posw = s.pos + w * Np;
       const uint64_t ek = world_key(p, wg0 + w, s.ep[w]);
       const int32_t turn = s.turn[w];
       uint32_t opos[kOMax];  // the ostriches' frame X|Y (after their acts: they act first)
@@ -340,23 +422,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         opos[k] = 0xFFFFFFFFu;
         hid_by[k] = 0xFFu;
         if (k < NO) {
-          const uint32_t pk = s.pos[k * kWorlds + w];
-          opos[k] = pk & 0xFFFFu;
-          if (k >= a0 && k < a1) {  // acts in this launch (phase A's W0 writes the same into hi16)
-            const int a = (int)(int8_t)A[w * na + k - a0];
-            const int2 xy = s.oxy[k * kWorlds + w];
-            opos[k] = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
-          }
+          opos[k] = (k >= a0 && k < a1) ? moved(s.omod[k * kWorlds + w], (int)(int8_t)A[w * na + k - a0], W, H)
+                                        : posw[k] & 0xFFFFu;
           const uint32_t ob = s.ost[k * kWorlds + w];
           vis |= (uint32_t)ost_visible(ob) << k;
           dead |= (uint32_t)(ost_status(ob) != 0) << k;
         }
       }
       for (int m = max(a0, NO); m < min(a1, NM); ++m) {
-        const int a = (int)(int8_t)A[w * na + m - a0];
-        const int2 xy = s.oxy[m * kWorlds + w];
-        const uint32_t np = (uint32_t)pymod(xy.x + move_dx(a), W) | ((uint32_t)pymod(xy.y + move_dy(a), H) << 8);
-        reinterpret_cast<uint16_t*>(&s.pos[m * kWorlds + w])[1] = (uint16_t)np;
+        const uint32_t np = moved(s.omod[m * kWorlds + w], (int)(int8_t)A[w * na + m - a0], W, H);
+        reinterpret_cast<uint16_t*>(posw + m)[1] = (uint16_t)np;
         uint32_t cand = 0;
 #pragma unroll
         for (int k = 0; k < kOMax; ++k) cand |= (uint32_t)((vis >> k & 1u) && opos[k] == np) << k;
@@ -389,19 +464,20 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       // the turn ends with this launch when its last entity acts; then the batched surface's
       // autoreset: every ostrich done, or max_turns reached
       const bool all_dead = NO > 0 && dead == (1u << NO) - 1u;
-      const bool rs = a1 == N && p.autoreset && (all_dead || (p.max_turns > 0 && turn + 1 >= p.max_turns));
+      const bool rs = a1 == N && na > 0 && p.autoreset && (all_dead || (p.max_turns > 0 && turn + 1 >= p.max_turns));
       s.ep_reset[w] = rs ? s.ep[w] + 1u : 0u;
       const bool valid = w < nvalid;
       if (p.world_reset && valid) p.world_reset[(int64_t)t * p.B + wg0 + w] = (uint8_t)rs;
       resets += (rs && valid) ? 1 : 0;
     } else if (wave == 2) {
       WAB2_PHASE_PARAMS;
-      // bushes act on nothing (World.py:9-10); their frame X/Y become x mod W, y mod H
+      // bushes act on nothing (World.py:9-10); their frame X/Y become x mod W, y mod H (own
+      // x in [0, W], y in [0, H])
       const int w = lane;
       for (int b = max(a0, NM) - NM; b < a1 - NM; ++b) {
         const uint32_t bxy = s.bxy[b * kWorlds + w];
-        const uint32_t np = (uint32_t)pymod((int)(bxy & 0xFFu), W) | ((uint32_t)pymod((int)(bxy >> 8), H) << 8);
-        reinterpret_cast<uint16_t*>(&s.pos[(NM + b) * kWorlds + w])[1] = (uint16_t)np;
+        const uint32_t np = (uint32_t)wrap1((int)(bxy & 0xFFu), W) | ((uint32_t)wrap1((int)(bxy >> 8), H) << 8);
+        reinterpret_cast<uint16_t*>(s.pos + w * Np + NM + b)[1] = (uint16_t)np;
       }
     } else if (t + 1 < T) {
       WAB2_PHASE_PARAMS;
@@ -423,8 +499,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       uint8_t* obs_t = p.obs + (int64_t)t * p.B * no * R;
       const bool whole_turn = a0 == 0 && a1 == N && o0 == 0 && no == N;
       const int hf = lane >> 5;
-      const int nd = (2 * N + 3) >> 2;  // delta dwords
-      const int bb = 24 + 2 * N;        // first bush-food byte
+      const int nd = (N + 1) >> 1;        // delta dwords
+      const int bb = 24 + 2 * N;          // first bush-food byte
+      const int nbp = (NB + 1) >> 1;      // bush-food byte pairs
       for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
         const int q = rnd * 32 + (lane & 31);
         const bool on = q < nitems;
@@ -432,53 +509,71 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const int w = (int)(((uint32_t)qc * p.magic_o) >> 20);
         const int i = o0 + qc - w * no;
         const int type = i < NO ? T_OSTRICH : i < NM ? T_WOLF : T_BUSH;
-        const uint32_t pi = s.pos[i * kWorlds + w];
-        const int ex = (int)(pi & 0xFFu), ey = (int)((pi >> 8) & 0xFFu);
+        const uint32_t* posw = s.pos + w * Np;
+        const uint32_t pi = posw[i];
+        View v;
+        v.ex = (int)(pi & 0xFFu);
+        v.ey = (int)((pi >> 8) & 0xFFu);
+        v.W = W;
+        v.H = H;
         const uint32_t ob = type == T_OSTRICH ? s.ost[i * kWorlds + w] : 0u;
         const int role = ost_role(ob), status = ost_status(ob);
         // World.get_observations (:365-374)
         const int r = type == T_OSTRICH ? (role == 1 ? p.rg : p.rl) : type == T_WOLF ? p.rw : 0;
         const int rc = min(r, 255);
-        const int r2 = rc * rc;  // (dx^2 + dy^2) ** 0.5 <= r  <=>  dx^2 + dy^2 <= r^2 (integers)
-        // the wrap of World.py:255-291 as thresholds on dx: the `if` side replaces dx by
-        // dx - W when X >= W - (r - x) and |dx - W| < |dx|; the `elif` side by dx + W
-        const int lox = ex < r ? W - r : 0x7FFF, hix = (ex >= r && W < ex + r) ? r - W : -0x7FFF;
-        const int loy = ey < r ? H - r : 0x7FFF, hiy = (ey >= r && H < ey + r) ? r - H : -0x7FFF;
+        v.r2 = rc * rc;  // (dx^2 + dy^2) ** 0.5 <= r  <=>  dx^2 + dy^2 <= r^2 (integers)
+        v.xl = v.ex < r ? max(W - r + v.ex, v.ex + W / 2 + 1) : 0x7FFF;
+        v.xr = (v.ex >= r && W < v.ex + r) ? min(r - W + v.ex, v.ex - W / 2 - 1) : -0x7FFF;
+        v.yl = v.ey < r ? max(H - r + v.ey, v.ey + H / 2 + 1) : 0x7FFF;
+        v.yr = (v.ey >= r && H < v.ey + r) ? min(r - H + v.ey, v.ey - H / 2 - 1) : -0x7FFF;
         // ostriches still Visible when i observes: visible before the launch and not hidden
         // by a wolf of this launch that acted before i
-        uint32_t alive = 0xFFFFFFFFu;
+        v.alive = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < kOMax; ++k)
           if (k < NO) {
             const uint32_t okb = s.ost[k * kWorlds + w];
             const int h = s.hid[k * kWorlds + w];
-            if (!ost_visible(okb) || h < i) alive &= ~(1u << k);
+            if (!ost_visible(okb) || h < i) v.alive &= ~(1u << k);
           }
         // entity j is where observer i sees it: after its act if it acted in this launch
         // before i (a0 <= j < i), else at its frame position from before the launch
         const int jn = min(i, a1);
-        uint32_t vis = 0, d[NMAX / 4];
+        uint32_t vis = 0, d[NKK];
+        uint2 pp[NKK];  // this lane's entities of the world, all loads issued before any use
 #pragma unroll
-        for (int kk = 0; kk < NMAX / 4; ++kk) {
-          d[kk] = 0;
+        for (int kk = 0; kk < NKK; ++kk) pp[kk] = *reinterpret_cast<const uint2*>(posw + 4 * kk + 2 * hf);
+#if WAB2_PACKED
+        View2 v2;
+        v2.e = (s16x2){(short)v.ex, (short)v.ey};
+        v2.lo = (s16x2){(short)min(v.xl, 0x4000), (short)min(v.yl, 0x4000)};
+        v2.hi = (s16x2){(short)max(v.xr, -0x4000), (short)max(v.yr, -0x4000)};
+        v2.wh = (s16x2){(short)W, (short)H};
+        v2.r2 = v.r2;
+        // rows of the frame: alive (the ostriches) and existing (j < N)
+        const uint32_t vmask = v.alive & (N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u) & (WAB2_ABLATE & 1 ? 0u : ~0u);
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int j = 4 * kk + 2 * hf + u;
-            if (j < N && !(WAB2_ABLATE & 1)) {
-              const uint32_t pj = s.pos[j * kWorlds + w];
-              const uint32_t xy = (j >= a0 && j < jn) ? pj >> 16 : pj & 0xFFFFu;
-              int dx = (int)(xy & 0xFFu) - ex, dy = (int)(xy >> 8) - ey;
-              dx = (dx >= lox && 2 * dx > W) ? dx - W : dx;
-              dx = (dx <= hix && 2 * dx < -W) ? dx + W : dx;
-              dy = (dy >= loy && 2 * dy > H) ? dy - H : dy;
-              dy = (dy <= hiy && 2 * dy < -H) ? dy + H : dy;
-              const bool ok = dx * dx + dy * dy <= r2 && (alive >> j & 1u);
-              vis |= (uint32_t)ok << j;
-              const uint32_t pair = ((uint32_t)dx & 0xFFu) | (((uint32_t)dy & 0xFFu) << 8);
-              d[kk] |= ok ? pair << (16 * u) : 0u;
-            }
-          }
+        for (int kk = 0; kk < NKK; ++kk) {
+          const int j = 4 * kk + 2 * hf;
+          const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
+          uint32_t ok0, ok1;
+          const uint32_t p0 = view_pair2(v2, (pp[kk].x >> s0) & 0xFFFFu, ok0);
+          const uint32_t p1 = view_pair2(v2, (pp[kk].y >> s1) & 0xFFFFu, ok1);
+          const uint32_t m = (vmask >> j) & (ok0 | (ok1 << 1));
+          vis |= m << j;
+          d[kk] = (p0 & (0u - (m & 1u))) | ((p1 << 16) & (0u - (m >> 1)));
         }
+#else
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) {
+          const int j = 4 * kk + 2 * hf;
+          // 16-bit shift by 16 where the entity acted before i in this launch (a0 <= j < i)
+          const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
+          const uint32_t x0 = (pp[kk].x >> s0) & 0xFFFFu, x1 = (pp[kk].y >> s1) & 0xFFFFu;
+          d[kk] = view_pair(v, x0, j, (uint32_t)(j < N) & (uint32_t)!(WAB2_ABLATE & 1), vis) |
+                  (view_pair(v, x1, j + 1, (uint32_t)(j + 1 < N) & (uint32_t)!(WAB2_ABLATE & 1), vis) << 16);
+        }
+#endif
         vis |= __shfl_xor(vis, 32);
         // internal obs (World.py:17-18, 50-51, 80-81)
         double food;
@@ -487,7 +582,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
           x = (int)(bxy & 0xFFu);
           y = (int)(bxy >> 8);
-          food = (double)s.bf1[(i - NM) * kWorlds + w];  // the bushes act after every ostrich
+          food = (double)s.bf1[w * NBp + i - NM];  // the bushes act after every ostrich
         } else {
           const int2 xy = s.oxy[i * kWorlds + w];
           x = xy.x;
@@ -511,25 +606,26 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           for (int z = 24 + 4 * nd; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
         }
 #pragma unroll
-        for (int kk = 0; kk < NMAX / 4; ++kk)
+        for (int kk = 0; kk < NKK; ++kk)
           if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
         // Additional_Data [food] of the visible bushes as the observer sees them: after the
-        // eats of the ostriches that acted before it in this launch
-        for (int b = hf; b < ((WAB2_ABLATE & 4) ? 0 : NB); b += 2) {
-          uint32_t f = 0;
-          if (vis >> (NM + b) & 1u) {
-            if (type == T_OSTRICH) {
-              f = s.bf0[b * kWorlds + w];
-              for (int k = a0; k < min(a1, NO); ++k)
-                if (k < i) {
-                  const uint32_t e = s.ev[k * kWorlds + w];
-                  if ((e & 0xFFu) == (uint32_t)b) f = e >> 8;
-                }
-            } else {
-              f = s.bf1[b * kWorlds + w];
-            }
+        // eats of the ostriches that acted before it in this launch (bf1 for every observer
+        // after the ostriches); byte pairs m = 2mm + half
+        for (int m = hf; m < ((WAB2_ABLATE & 4) ? 0 : nbp); m += 2) {
+          const int b = 2 * m;
+          const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
+          uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
+          if (type == T_OSTRICH) {
+            for (int k = a0; k < min(a1, NO); ++k)
+              if (k < i) {
+                const uint32_t e = s.ev[k * kWorlds + w];
+                if ((e & 0xFFu) == (uint32_t)b) f = (f & 0xFF00u) | (e >> 8);
+                if ((e & 0xFFu) == (uint32_t)b + 1u) f = (f & 0x00FFu) | (e & 0xFF00u);
+              }
           }
-          rec[bb + b] = (uint8_t)f;
+          const uint32_t vb = vis >> (NM + b);
+          f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
+          *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -540,8 +636,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const int chunks = cnt * R / 16;
         uint8_t* dst = obs_t + (item0 + q0) * (int64_t)R;
         for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(stage + 16 * c);
-          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + 16 * c));
+          const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
+          __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(dst + 16 * c));
         }
         __builtin_amdgcn_wave_barrier();
       }
@@ -558,7 +654,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const int e = q >> 6, w = q & 63;
         const uint32_t epr = s.ep_reset[w];
         const bool acts = e >= a0 && e < a1;
-        if (acts) s.pos[e * kWorlds + w] >>= 16;  // the frame X/Y after the act (a reset leaves it)
+        if (acts) s.pos[w * Np + e] >>= 16;  // the frame X/Y after the act (a reset leaves it)
         const int a = acts ? (int)(int8_t)A[w * na + e - a0] : -1;
         int nx = 0, ny = 0;
         if (epr) {  // reset_environment: randint(0, W), randint(0, H) (WAB_Environment2_Single.py:45-46)
@@ -570,6 +666,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           int2 xy = s.oxy[e * kWorlds + w];
           xy.x += move_dx(a);
           xy.y += move_dy(a);
+          uint32_t om = acts ? moved(s.omod[e * kWorlds + w], a, W, H) : s.omod[e * kWorlds + w];
           double f = s.food[e * kWorlds + w];
           const uint32_t g = acts ? s.gain[e * kWorlds + w] : 0u;
           const uint32_t ob0 = e < NO ? s.ost[e * kWorlds + w] : 0u;  // before this launch's kills
@@ -596,12 +693,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             p.reward[(int64_t)(wg0 + w) * na + e - a0] = rew;
             p.done[(int64_t)(wg0 + w) * na + e - a0] = dn;
           }
-          if (epr) xy = make_int2(nx, ny);
+          if (epr) {
+            xy = make_int2(nx, ny);
+            om = (uint32_t)wrap1(nx, W) | ((uint32_t)wrap1(ny, H) << 8);
+          }
           s.oxy[e * kWorlds + w] = xy;
+          s.omod[e * kWorlds + w] = (uint16_t)om;
           s.food[e * kWorlds + w] = f;
         } else {
           const int b = e - NM;
-          s.bf0[b * kWorlds + w] = epr ? (uint8_t)p.fpb : s.bf1[b * kWorlds + w];
+          s.bf0[w * NBp + b] = epr ? (uint8_t)p.fpb : s.bf1[w * NBp + b];
           if (epr) s.bxy[b * kWorlds + w] = (uint16_t)(nx | (ny << 8));
           if (!whole_turn && acts && w < nvalid) {
             p.reward[(int64_t)(wg0 + w) * na + e - a0] = 0.0f;
@@ -623,7 +724,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     for (int q = tid; q < nent; q += kThreads) {
       const int e = q >> 6, w = q & 63;
       const int64_t a = (int64_t)e * p.Bp + wg0 + w;
-      p.df[a] = (uint16_t)s.pos[e * kWorlds + w];
+      p.df[a] = (uint16_t)s.pos[w * Np + e];
       if (e < NM) {
         const int2 xy = s.oxy[e * kWorlds + w];
         p.ox[a] = xy.x;
@@ -634,7 +735,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const uint32_t bxy = s.bxy[b * kWorlds + w];
         p.ox[a] = (int32_t)(bxy & 0xFFu);
         p.oy[a] = (int32_t)(bxy >> 8);
-        p.bfood[(int64_t)b * p.Bp + wg0 + w] = s.bf0[b * kWorlds + w];
+        p.bfood[(int64_t)b * p.Bp + wg0 + w] = s.bf0[w * NBp + b];
       }
       if (e < NO) p.ost[(int64_t)e * p.Bp + wg0 + w] = s.ost[e * kWorlds + w];
       if (e == 0) {
@@ -759,6 +860,34 @@ std::string validate(const wab2_config* c) {
   return "";
 }
 
+// the kernel instantiation for N entities: ceil(N / 4) dword-pair groups of the delta array
+const void* torus_kernel(int N) {
+  switch ((N + 3) / 4) {
+    case 1: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<1>);
+    case 2: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<2>);
+    case 3: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<3>);
+    case 4: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<4>);
+    case 5: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<5>);
+    case 6: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<6>);
+    case 7: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<7>);
+    default: return reinterpret_cast<const void*>(&wab2::wab_torus_kernel<8>);
+  }
+}
+
+void launch_torus(const wab2_handle* h, const TParams& p, hipStream_t stream) {
+  const dim3 grid((unsigned)h->n_blocks), block(wab2::kThreads);
+  switch ((p.N + 3) / 4) {
+    case 1: hipLaunchKernelGGL(wab2::wab_torus_kernel<1>, grid, block, h->lds, stream, p); break;
+    case 2: hipLaunchKernelGGL(wab2::wab_torus_kernel<2>, grid, block, h->lds, stream, p); break;
+    case 3: hipLaunchKernelGGL(wab2::wab_torus_kernel<3>, grid, block, h->lds, stream, p); break;
+    case 4: hipLaunchKernelGGL(wab2::wab_torus_kernel<4>, grid, block, h->lds, stream, p); break;
+    case 5: hipLaunchKernelGGL(wab2::wab_torus_kernel<5>, grid, block, h->lds, stream, p); break;
+    case 6: hipLaunchKernelGGL(wab2::wab_torus_kernel<6>, grid, block, h->lds, stream, p); break;
+    case 7: hipLaunchKernelGGL(wab2::wab_torus_kernel<7>, grid, block, h->lds, stream, p); break;
+    default: hipLaunchKernelGGL(wab2::wab_torus_kernel<8>, grid, block, h->lds, stream, p); break;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -832,8 +961,7 @@ int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t wo
   if (e == hipSuccess) { e = alloc(&q, NBp * 4); p.episode = (uint32_t*)q; }
   if (e == hipSuccess) { e = alloc(&q, 2 * sizeof(unsigned long long)); p.counters = (unsigned long long*)q; }
   if (e == hipSuccess && h->lds > 64 * 1024)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wab2::wab_torus_kernel<wab2::kNMax>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+    e = hipFuncSetAttribute(torus_kernel(p.N), hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(wab2::wab_torus_create_kernel, dim3((unsigned)((p.Bp + 255) / 256)), dim3(256), 0, 0, p);
     e = hipGetLastError();
@@ -892,8 +1020,7 @@ int wab2_rollout(wab2_handle* h, const int8_t* actions, int32_t T, uint8_t* obs,
   p.done = done;
   p.world_reset = world_reset;
   p.act_scalar = ((reinterpret_cast<uintptr_t>(actions) & 3u) == 0u && (p.B * p.N) % 4 == 0) ? 1 : 0;
-  hipLaunchKernelGGL(wab2::wab_torus_kernel<wab2::kNMax>, dim3((unsigned)h->n_blocks), dim3(wab2::kThreads), h->lds,
-                     (hipStream_t)stream, p);
+  launch_torus(h, p, (hipStream_t)stream);
   HIP_TRY2(hipGetLastError());
   return WAB2_OK;
 }
@@ -922,8 +1049,7 @@ int wab2_get_obs(wab2_handle* h, int32_t entity, uint8_t* obs, void* stream) {
   p.reward = nullptr;
   p.done = nullptr;
   p.world_reset = nullptr;
-  hipLaunchKernelGGL(wab2::wab_torus_kernel<wab2::kNMax>, dim3((unsigned)h->n_blocks), dim3(wab2::kThreads), h->lds,
-                     (hipStream_t)stream, p);
+  launch_torus(h, p, (hipStream_t)stream);
   HIP_TRY2(hipGetLastError());
   return WAB2_OK;
 }
@@ -946,8 +1072,7 @@ int wab2_take_action(wab2_handle* h, int32_t entity, const int8_t* actions, floa
   p.reward = reward;
   p.done = done;
   p.world_reset = world_reset;
-  hipLaunchKernelGGL(wab2::wab_torus_kernel<wab2::kNMax>, dim3((unsigned)h->n_blocks), dim3(wab2::kThreads), h->lds,
-                     (hipStream_t)stream, p);
+  launch_torus(h, p, (hipStream_t)stream);
   HIP_TRY2(hipGetLastError());
   h->next_entity = (entity + 1) % h->p.N;
   return WAB2_OK;
