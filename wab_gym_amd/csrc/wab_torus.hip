@@ -306,7 +306,8 @@ __device__ __forceinline__ s16x2 unpack_xy(uint32_t xy) {
 // (the compiler otherwise splits `x >> 15` of a short2 into per-half compares and selects)
 __device__ __forceinline__ s16x2 sign_mask2(s16x2 x) {
   uint32_t r, v = __builtin_bit_cast(uint32_t, x);
-  asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(r) : "v"(v));
+  // op_sel_hi:[0,1]: the high half also shifts by the constant's low 16 bits (15)
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(v));
   return __builtin_bit_cast(s16x2, r);
 }
 
