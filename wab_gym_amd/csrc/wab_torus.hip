@@ -23,6 +23,8 @@
 //            instruction writes 1 KiB contiguous;
 //   phase C  the turn's end, one lane per (entity, world): positions, roles, status,
 //            Visible, food, autoreset draws.
+// The waves exchange data only through LDS, so the phase barriers are LDS-only
+// (wab::lds_barrier): __syncthreads() would also wait for every record store in flight.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -220,26 +222,25 @@ __device__ __forceinline__ TParams kparams(const TParams& p0) {
 #endif
 }
 
-// actions of turn t for the workgroup's worlds into act (raw [64][N] bytes).  Scalar loads
-// (counted in lgkmcnt, so nothing waits on the wave's stores) when the slice is 4-byte aligned
-// and the workgroup is full; per-byte vector loads otherwise.
+// actions of turn t for the workgroup's worlds into act (raw [64][N] bytes), by one wave:
+// dword loads, all issued before the first is used, when the slice is 4-byte aligned and the
+// workgroup is full (the wave's stores of the previous turn, which the same vmcnt counts, are
+// long retired by then); per-byte loads otherwise.
 __device__ __forceinline__ void fetch_actions_wave(const TParams& p, int t, int64_t wg0, int nvalid, uint8_t* act,
                                                    int lane) {
   const int nbytes = kWorlds * p.N;
   const int8_t* src = p.actions + (int64_t)t * p.B * p.N + wg0 * p.N;
   if (p.act_scalar && nvalid == kWorlds) {
-    typedef const uint32_t __attribute__((address_space(4))) CU32;
-    CU32* c = (CU32*)reinterpret_cast<uintptr_t>(src);
-    asm volatile("" : "+s"(c));
-    for (int ch = 0; ch < nbytes / 64; ++ch) {  // 64-byte chunks (64 * N is a multiple of 64)
-      uint32_t v[16];
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(act);
+    constexpr int kMax = (WAB2_MAX_ENTITIES * kWorlds / 4 + 63) / 64;  // dwords per lane, at most 8
+    uint32_t v[kMax];
+    const int nd = nbytes / 4;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = c[ch * 16 + k];
-      uint32_t d = 0;
+    for (int k = 0; k < kMax; ++k) v[k] = lane + 64 * k < nd ? s32[lane + 64 * k] : 0u;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) d = lane == k ? v[k] : d;
-      if (lane < 16) reinterpret_cast<uint32_t*>(act)[ch * 16 + lane] = d;
-    }
+    for (int k = 0; k < kMax; ++k)
+      if (lane + 64 * k < nd) d32[lane + 64 * k] = v[k];
   } else {
     for (int q = lane; q < nbytes; q += 64)
       act[q] = q < nvalid * p.N ? (uint8_t)src[q] : (uint8_t)0;
@@ -366,7 +367,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     const int8_t* src = p.actions + wg0 * na;
     for (int q = tid; q < kWorlds * na; q += kThreads) s.act0[q] = q < nvalid * na ? (uint8_t)src[q] : (uint8_t)0;
   }
-  __syncthreads();
+  lds_barrier();
 
   int64_t resets = 0;
   for (int t = 0; t < T; ++t) {
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       WAB2_PHASE_PARAMS;
       fetch_actions_wave(p, t + 1, wg0, nvalid, (t & 1) ? s.act0 : s.act1, lane);
     }
-    __syncthreads();
+    lds_barrier();
 
     // ================= phase B: observation records (and, for a whole turn, reward and done).
     // Rounds of 32 (world, observer) items per wave; lanes l and l + 32 share item l: each
@@ -643,7 +644,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         __builtin_amdgcn_wave_barrier();
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ================= phase C: the launch's end, one lane per (entity, world): the acting
     // entities' moves, roles and food, every ostrich's kills, the bushes' food, the autoreset
@@ -716,7 +717,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   // ---- epilogue: LDS tables -> state
