@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define WAB_ABI_VERSION 4
+#define WAB_ABI_VERSION 5
 #define WAB_MAX_WOLF_SLOTS 32 /* largest per-env live-wolf slot count (wab_config.wolf_slots) */
 #define WAB_MAX_VIEW 63       /* largest odd width/height accepted */
 
@@ -130,6 +130,10 @@ typedef struct wab_counters {
                               * guard; nonzero means results are invalid; must stay 0) */
   uint64_t wolf_overflow_reset; /* the part of wolf_overflow dropped by resets (a new episode's
                                  * initial wolves beyond the slots); the rest are ring spawns */
+  uint64_t rollout_launches;   /* wab_rollout / wab_rollout_features calls that ran as ONE launch
+                                * (host-side tally) */
+  uint64_t rollout_step_calls; /* ... that ran as T per-step calls instead (misaligned plane
+                                * slices, other kernels; host-side tally) */
 } wab_counters;
 
 typedef struct wab_handle wab_handle;
@@ -215,9 +219,9 @@ int64_t wab_batch(const wab_handle* h);
 int wab_set_obs_placement(wab_handle* h, int32_t placement);
 
 /* Name of the kernel wab_step launches for this handle: "small" (the four-wave kernel for
- * views of at most 128 cells in unpadded rows), "wide" (views of at most 32x32 cells in rows
- * of 16 or 32 bytes, without restrict_view: the 31x31 configuration) or "block" (the general
- * one).  Diagnostics only. */
+ * views of at most 128 cells in unpadded rows), "wide" (width <= 31 and height <= 32, in rows
+ * of 16 or 32 bytes, without restrict_view: the 31x31 configuration; width 32 steps on "block")
+ * or "block" (the general one).  Diagnostics only. */
 const char* wab_step_kernel(const wab_handle* h);
 
 /* ---- config 5 (actor_critic.py rollout) ------------------------------------------ */

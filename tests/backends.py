@@ -86,3 +86,34 @@ class GpuRolloutBackend:
 
     def state(self):
         return self.env.state()
+
+
+class GpuPaddedRolloutBackend(GpuRolloutBackend):
+    """GpuRolloutBackend over a batch padded to a multiple of 16 envs (extra envs get ids after
+    the group's and action 0; their results are dropped), so that every step's plane slice is
+    16-byte aligned and wab_rollout takes its one-launch path for the small and wide kernels:
+    asserted from the handle's host tallies after every rollout."""
+
+    def __init__(self, opts, base, n, autoreset, stride, seed=SEED):
+        self.n = n
+        super().__init__(opts, base, -(-n // 16) * 16, autoreset, stride, seed)
+        self.one_launch = self.env.step_kernel in ("small", "wide")
+
+    def reset(self):
+        return tuple(x[:self.n] for x in super().reset())
+
+    def rollout(self, actions):
+        a = np.zeros((len(actions), self.env.num_envs), np.int64)
+        a[:, :self.n] = actions
+        before = self.env.counters()
+        out = tuple(x[:, :self.n] for x in super().rollout(a))
+        c = self.env.counters()
+        launches = c["rollout_launches"] - before["rollout_launches"]
+        per_step = c["rollout_step_calls"] - before["rollout_step_calls"]
+        assert (launches, per_step) == ((1, 0) if self.one_launch else (0, 1)), (
+            "rollout of %d envs (%s kernel) ran %d one-launch / %d per-step calls"
+            % (self.env.num_envs, self.env.step_kernel, launches, per_step))
+        return out
+
+    def state(self):
+        return {k: v[:self.n] for k, v in self.env.state().items()}

@@ -31,10 +31,32 @@ def test_gpu_matches_reference_golden(name):
 @pytest.mark.parametrize("name", gr.SETS)
 def test_gpu_rollout_matches_reference_golden(name):
     """Every golden set through env.rollout (wab_rollout: the multi-step launches bench.py
-    times), in consecutive rollouts of 1, 7 and 64 steps with the state carried across them."""
+    times), in consecutive rollouts of 1, 7 and 64 steps with the state carried across them.
+    Each group is padded to a multiple of 16 envs so that its plane slices are 16-byte aligned:
+    the backend asserts that every rollout ran as the ONE launch bench.py times."""
+    from backends import GpuPaddedRolloutBackend
+
+    assert gr.replay_rollout(name, GpuPaddedRolloutBackend) > 0
+
+
+def test_gpu_rollout_golden_misaligned_falls_back_per_step():
+    """The golden groups as they are (40 and 1 envs of 363-byte planes: misaligned step slices)
+    take wab_rollout's per-step path through the handle's scratch planes; same results."""
     from backends import GpuRolloutBackend
 
-    assert gr.replay_rollout(name, GpuRolloutBackend) > 0
+    seen = []
+
+    class Tally(GpuRolloutBackend):
+        def rollout(self, actions):
+            before = self.env.counters()
+            out = super().rollout(actions)
+            c = self.env.counters()
+            seen.append((c["rollout_launches"] - before["rollout_launches"],
+                         c["rollout_step_calls"] - before["rollout_step_calls"]))
+            return out
+
+    assert gr.replay_rollout("default", Tally) > 0
+    assert seen and all(x == (0, 1) for x in seen), seen
 
 
 def test_gpu_rollout_golden_wide_kernel_and_8_slots():
@@ -131,10 +153,20 @@ def test_c3_batch65536_wide31_padded_lockstep(return_terminal):
 ])
 @pytest.mark.parametrize("return_terminal", [True, False])
 def test_wide_kernel_lockstep(opts, stride, slots, autoreset, return_terminal):
-    """The wide-view kernel (W, H <= 32, rows of 16 or 32 bytes) against the oracle."""
+    """The wide-view kernel (width <= 31, height <= 32, rows of 16 or 32 bytes) against the oracle."""
     env, _ = _lockstep(opts, 1000, 120, autoreset=autoreset, stride=stride, wolf_slots=slots, base=5,
                        return_terminal=return_terminal)
     assert env.step_kernel == "wide"
+
+
+@pytest.mark.parametrize("width,height,kernel", [(31, 31, "wide"), (33, 31, "block"), (31, 33, "block")])
+def test_wide_kernel_width_limit(width, height, kernel):
+    """The wide kernel takes width <= 31 and height <= 32 (wab_capi.hip wide_view; sizes are
+    odd, wab_env.py:147-148, so 31 is the largest): 33 either way in 32- or 48-byte rows steps
+    on the block kernel, still equal to the oracle."""
+    env, _ = _lockstep({"width": width, "height": height}, 200, 40, stride=32 if height <= 32 else 48,
+                       wolf_slots=16)
+    assert env.step_kernel == kernel
 
 
 def test_wide_kernel_reset_mask():

@@ -28,7 +28,7 @@ EXPORTED = [
 ABI2_VERSION = 1
 OBS_SAME_BUFFER, OBS_FRESH_BUFFER = 0, 1  # wab_set_obs_placement
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class WabObs(ctypes.Structure):
@@ -40,7 +40,8 @@ class WabCounters(ctypes.Structure):
     _fields_ = [("wolf_overflow", ctypes.c_uint64), ("eaten_overflow", ctypes.c_uint64),
                 ("bad_actions", ctypes.c_uint64), ("steps", ctypes.c_uint64),
                 ("resets", ctypes.c_uint64), ("ego_missing", ctypes.c_uint64),
-                ("handoff_timeouts", ctypes.c_uint64), ("wolf_overflow_reset", ctypes.c_uint64)]
+                ("handoff_timeouts", ctypes.c_uint64), ("wolf_overflow_reset", ctypes.c_uint64),
+                ("rollout_launches", ctypes.c_uint64), ("rollout_step_calls", ctypes.c_uint64)]
 
 
 class WabError(RuntimeError):

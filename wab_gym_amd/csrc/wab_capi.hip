@@ -61,6 +61,7 @@ struct wab_handle {
   size_t wide_lds_bytes = 0;  // LDS per workgroup of the wide kernel (see wab_create)
   size_t wide_roll_lds_bytes = 0;  // ... of its multi-step build (wab_rollout_wide)
   int32_t obs_placement = WAB_OBS_SAME_BUFFER;  // wab_set_obs_placement: which wide per-step build
+  uint64_t rollout_launches = 0, rollout_step_calls = 0;  // wab_counters' host tallies
 };
 
 namespace {
@@ -133,8 +134,8 @@ bool small_map(const Params& p) { return p.WHW <= 4; }
 // Step kernels.  The block kernel (wab_step.hip) handles every configuration; views whose
 // planes fit 128 bits (W*H <= 128, unpadded rows, spawn ring <= 128 tiles, restrict_view only
 // at exactly 11x11) step with the four-wave small-view kernel (wab_step_small.hip); other
-// views of at most 32 x 32 cells in rows of 16 or 32 bytes without restrict_view step and
-// reset with the wide-view kernel (wab_step_wide.hip, its own bitmap layout: one dword per
+// views of width <= 31 and height <= 32 in rows of 16 or 32 bytes without restrict_view step
+// and reset with the wide-view kernel (wab_step_wide.hip, its own bitmap layout: one dword per
 // row).
 enum { KERNEL_BLOCK = 0, KERNEL_SMALL = 1, KERNEL_WIDE = 2 };
 
@@ -729,6 +730,7 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
     p.done = done;
     p.n_steps = T;
     DeviceGuard guard(h->device);
+    ++h->rollout_launches;
     if (h->step_kernel == KERNEL_WIDE) {
       if (h->n_blocks == 0) return WAB_OK;
       hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_roll_lds_bytes,
@@ -738,6 +740,7 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
     }
     return launch<0>(h, p, (hipStream_t)stream);
   }
+  if (T > 0) ++h->rollout_step_calls;
   for (int32_t t = 0; t < T; ++t) {
     wab_obs o;
     uint8_t* dst = obs_seq->planes + (size_t)t * (size_t)B * OB;
@@ -778,6 +781,8 @@ int wab_get_counters(wab_handle* h, wab_counters* out, void* stream) {
   out->wolf_overflow_reset = c[wab::CTR_WOLF_OVERFLOW_RESET];
   out->resets = 0;
   for (size_t i = 0; i < br.size(); ++i) out->resets += br[i];
+  out->rollout_launches = h->rollout_launches;
+  out->rollout_step_calls = h->rollout_step_calls;
   return WAB_OK;
 }
 
@@ -959,11 +964,13 @@ int wab_rollout_features(wab_handle* h, const int8_t* actions, int32_t T, const 
       p.gamma = gamma;
     }
     DeviceGuard guard(h->device);
+    ++h->rollout_launches;
     if (h->small_g11) launch_small<11, true, true>(h, p, (hipStream_t)stream, roll_lds);
     else launch_small<0, true, true>(h, p, (hipStream_t)stream, roll_lds);
     HIP_TRY(hipGetLastError());
     if (fused_returns) return WAB_OK;
   } else {
+    ++h->rollout_step_calls;
     for (int32_t t = 0; t < T; ++t) {  // (no fused kernel for these options: T fused-or-not steps)
       wab_obs o;
       o.planes = obs_seq->planes ? obs_seq->planes + (size_t)t * (size_t)B * OB : nullptr;

@@ -325,7 +325,9 @@ constexpr int kW1ResetPrio = 2;
 // co-resident workgroups of a CU (blockIdx b, b + 256, ...: at equal priority the arbiter
 // favours the oldest): C5 T = 64 23.84-23.87 -> 23.36-23.37 us per step; the plain rollout
 // measured slower with it (5.70-5.75 -> 5.93-5.94), and with the four levels rotating, role
-// ignored (C5 23.74-23.75, default 5.95-5.97).
+// ignored (C5 23.74-23.75, default 5.95-5.97).  blockIdx >> 8 is the dispatch round on
+// MI355X's 256 CUs (one workgroup per CU per round); on a part with another CU count it is a
+// different partition of the groups: a scheduling hint only, results do not depend on it.
 template <bool ROLL>
 __device__ __forceinline__ void role_prio(uint32_t level, int t, bool rot) {
   if (ROLL && rot)

@@ -1618,7 +1618,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
       // rotating: 1965, 2070, 2174, 2304).  C3 T = 64: 2728-2737 -> 2618-2628 us per launch
       // (tools/ab_wide.sh; every wave rotating: 2609-2633; static inverse-age priority 2786).
       // (one-step launches: priority = age, the youngest first; 59.1 us per step into a ring,
-      // against 63.2 at priority 0 and 63.5 oldest first)
+      // against 63.2 at priority 0 and 63.5 oldest first).  The 256 is MI355X's CU count
+      // (one group per CU per dispatch round); elsewhere only the hint changes, not results.
       set_prio_dyn(((blockIdx.x >> 8) + (uint32_t)t) & 3u);
       if (wave == 2 && t == 0) {
         copy_to_lds(ring, p.tables + p.ring_at, (p.R + 3) & ~3, lane);

@@ -89,6 +89,7 @@ class BatchedWolvesAndBushesEnv:
         self._zero_mask = torch.zeros((11, 11), **u8)
         self._reset_once = False
         self._planes_valid = True  # False while the obs planes buffer is stale (planes not stored)
+        self._pending_planes = None  # rollout()'s last-step planes, copied into _obs on first use
         self.n_actions = n_actions(opts)
         self.action_space = Discrete(self.n_actions)  # wab_env.py:188-191
         W, H = self.W, self.H
@@ -152,6 +153,7 @@ class BatchedWolvesAndBushesEnv:
         if mask is not None:
             if not self._reset_once:
                 raise RuntimeError("the first reset must cover every env (mask=None)")
+            self._materialize_planes()  # (a masked reset rewrites only the masked envs' planes)
             m = t.as_tensor(mask, device=self.device).to(t.uint8).contiguous()
             if m.shape != (self.num_envs,):
                 raise ValueError("mask must have shape [num_envs]")
@@ -162,6 +164,7 @@ class BatchedWolvesAndBushesEnv:
         self._reset_once = True
         if m is None:
             self._planes_valid = True
+            self._pending_planes = None
         return self._obs_tuple(self._obs)
 
     def _step_actions(self, actions):
@@ -252,6 +255,7 @@ class BatchedWolvesAndBushesEnv:
                                         self.reward.data_ptr(), self.done.data_ptr(), term,
                                         self._stream()), "wab_step")
         self._planes_valid = True
+        self._pending_planes = None
         info = {}
         if self._term is not None:
             info["terminal_obs"] = self._obs_tuple(self._term)
@@ -271,11 +275,16 @@ class BatchedWolvesAndBushesEnv:
                                                  features.data_ptr(), self._stream()),
                    "wab_step_features")
         self._planes_valid = bool(store_planes)
+        self._pending_planes = None
         return features, self.reward, self.done.view(self._torch.bool)
 
     def rollout(self, actions):
         """T fused steps: actions [T, B] -> (planes [T,B,3,W,S], scalars [T,3,B], reward [T,B],
-        done [T,B]).  Equivalent to T step() calls without terminal observations."""
+        done [T,B]).  Equivalent to T step() calls without terminal observations: the env's
+        scalars, reward and done show the last step afterwards; its own obs planes show it too,
+        copied from planes[T-1] only when first needed (render(), the wrappers' observation(),
+        a masked reset), so modify the returned planes in place only after that or a later
+        step()/reset().  terminal_observation is not updated (it keeps the last step()'s)."""
         t = self._torch
         a = t.as_tensor(actions, device=self.device)
         if a.dim() != 2 or a.shape[1] != self.num_envs:
@@ -294,8 +303,8 @@ class BatchedWolvesAndBushesEnv:
                                            rew.data_ptr(), done.data_ptr(), self._stream()),
                    "wab_rollout")
         if T > 0:  # the env's buffers show the last step, as after T step() calls
-            self._obs["planes"].copy_(planes[T - 1])
             self._sync_last_step(scal[:, T - 1], rew[T - 1], done[T - 1])
+            self._pending_planes = planes[T - 1]
         return planes, scal.permute(1, 0, 2), rew, done
 
     def _sync_last_step(self, scal, rew, done):
@@ -357,9 +366,10 @@ class BatchedWolvesAndBushesEnv:
             # render() of the env's own buffer then raise)
             self._sync_last_step(scal[:, T - 1], rew[T - 1], done[T - 1])
             if planes is not None:
-                self._obs["planes"].copy_(planes[T - 1])
+                self._pending_planes = planes[T - 1]
             else:
                 self._planes_valid = False
+                self._pending_planes = None
         return {"features": features, "scalars": scal.permute(1, 0, 2), "reward": rew, "done": done,
                 "returns": ret, "planes": planes}
 
@@ -392,7 +402,13 @@ class BatchedWolvesAndBushesEnv:
         del keep
         return img
 
+    def _materialize_planes(self):
+        if self._pending_planes is not None:
+            self._obs["planes"].copy_(self._pending_planes)
+            self._pending_planes = None
+
     def _require_planes(self):
+        self._materialize_planes()
         if not self._planes_valid:
             raise RuntimeError("the env's obs planes were not stored by the last call "
                                "(step_features/rollout_features with store_planes=False); pass obs= "
