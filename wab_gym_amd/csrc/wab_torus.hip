@@ -27,6 +27,7 @@
 // (wab::lds_barrier): __syncthreads() would also wait for every record store in flight.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -92,7 +93,9 @@ struct TParams {
   // order, and the records of observers [o0, o1) are written, each as it observes before its
   // own act (wab2_get_obs: o = [i, i + 1), nothing acts; wab2_take_action: a = [i, i + 1))
   int32_t a0, a1, o0, o1;
-  uint32_t magic_o;       // ceil(2^20 / (o1 - o0)): q / (o1 - o0) for q < 2048
+  // (set by launch_torus) ceil(2^20 / n) for the window's n mover and n bush observers, so
+  // that q / n = (q * magic) >> 20 for q < 2048; ceil(2^16 / (R / 16))
+  uint32_t magic_m, magic_b, magic_cr;
 };
 
 __device__ __forceinline__ int pymod(int a, int m) {
@@ -488,160 +491,191 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     lds_barrier();
 
     // ================= phase B: observation records (and, for a whole turn, reward and done).
-    // Rounds of 32 (world, observer) items per wave; lanes l and l + 32 share item l: each
-    // computes half of the observer's view (delta dwords k = 2kk + half, i.e. entities
-    // 4kk + 2 half + {0, 1}), so a round's 32 records fit the wave's LDS stage and every lane
-    // is busy
+    // Two classes of observers, each in rounds of 32 (world, observer) items per wave: the
+    // movers (ostriches, wolves), whose view has a radius, and the bushes, whose radius is 0
+    // (World.py:365-374): a bush sees the rows on its own tile, at delta (0, 0), so its items take
+    // an equality test per entity and no view arithmetic, and never share a round (and its
+    // divergent paths) with a mover.  Lanes l and l + 32 share item l: each computes half of the
+    // observer's view (delta dwords k = 2kk + half, i.e. entities 4kk + 2 half + {0, 1}), so a
+    // round's 32 records fit the wave's LDS stage and every lane is busy.
     {
       WAB2_PHASE_PARAMS;
       const int o0 = p.o0, no = p.o1 - p.o0;
-      const int nitems = nvalid * no;
       uint8_t* stage = s.stage + wave * 32 * R;
-      const int64_t item0 = wg0 * no;  // first item of the workgroup in [B][no]
+      const int64_t item0 = wg0 * no;  // first record of the workgroup in [B][no]
       uint8_t* obs_t = p.obs + (int64_t)t * p.B * no * R;
       const bool whole_turn = a0 == 0 && a1 == N && o0 == 0 && no == N;
       const int hf = lane >> 5;
       const int nd = (N + 1) >> 1;        // delta dwords
       const int bb = 24 + 2 * N;          // first bush-food byte
       const int nbp = (NB + 1) >> 1;      // bush-food byte pairs
-      for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
-        const int q = rnd * 32 + (lane & 31);
-        const bool on = q < nitems;
-        const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
-        const int w = (int)(((uint32_t)qc * p.magic_o) >> 20);
-        const int i = o0 + qc - w * no;
-        const int type = i < NO ? T_OSTRICH : i < NM ? T_WOLF : T_BUSH;
-        const uint32_t* posw = s.pos + w * Np;
-        const uint32_t pi = posw[i];
-        View v;
-        v.ex = (int)(pi & 0xFFu);
-        v.ey = (int)((pi >> 8) & 0xFFu);
-        v.W = W;
-        v.H = H;
-        const uint32_t ob = type == T_OSTRICH ? s.ost[i * kWorlds + w] : 0u;
-        const int role = ost_role(ob), status = ost_status(ob);
-        // World.get_observations (:365-374)
-        const int r = type == T_OSTRICH ? (role == 1 ? p.rg : p.rl) : type == T_WOLF ? p.rw : 0;
-        const int rc = min(r, 255);
-        v.r2 = rc * rc;  // (dx^2 + dy^2) ** 0.5 <= r  <=>  dx^2 + dy^2 <= r^2 (integers)
-        v.xl = v.ex < r ? max(W - r + v.ex, v.ex + W / 2 + 1) : 0x7FFF;
-        v.xr = (v.ex >= r && W < v.ex + r) ? min(r - W + v.ex, v.ex - W / 2 - 1) : -0x7FFF;
-        v.yl = v.ey < r ? max(H - r + v.ey, v.ey + H / 2 + 1) : 0x7FFF;
-        v.yr = (v.ey >= r && H < v.ey + r) ? min(r - H + v.ey, v.ey - H / 2 - 1) : -0x7FFF;
-        // ostriches still Visible when i observes: visible before the launch and not hidden
-        // by a wolf of this launch that acted before i
-        v.alive = 0xFFFFFFFFu;
+      const int CR = R >> 4;              // 16-byte chunks per record
+      const uint32_t exist = N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u;
 #pragma unroll
-        for (int k = 0; k < kOMax; ++k)
-          if (k < NO) {
-            const uint32_t okb = s.ost[k * kWorlds + w];
-            const int h = s.hid[k * kWorlds + w];
-            if (!ost_visible(okb) || h < i) v.alive &= ~(1u << k);
-          }
-        // entity j is where observer i sees it: after its act if it acted in this launch
-        // before i (a0 <= j < i), else at its frame position from before the launch
-        const int jn = min(i, a1);
-        uint32_t vis = 0, d[NKK];
-        uint2 pp[NKK];  // this lane's entities of the world, all loads issued before any use
+      for (int cls = 0; cls < 2; ++cls) {
+        const bool bush = cls == 1;
+        // the class's observers [c0, c1) of the window
+        const int c0 = bush ? max(o0, NM) : o0, c1 = bush ? p.o1 : min(p.o1, NM);
+        const int nc = max(0, c1 - c0);
+        const uint32_t magic = bush ? p.magic_b : p.magic_m;  // q / nc = (q * magic) >> 20
+        const int nitems = nvalid * nc;
+        for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
+          const int q = rnd * 32 + (lane & 31);
+          const bool on = q < nitems;
+          const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
+          const int w = (int)(((uint32_t)qc * magic) >> 20);
+          const int i = c0 + qc - w * nc;
+          const int type = i < NO ? T_OSTRICH : i < NM ? T_WOLF : T_BUSH;
+          const uint32_t* posw = s.pos + w * Np;
+          const uint32_t pi = posw[i];
+          const uint32_t ob = (!bush && type == T_OSTRICH) ? s.ost[i * kWorlds + w] : 0u;
+          const int role = ost_role(ob), status = ost_status(ob);
+          // ostriches still Visible when i observes: visible before the launch and not hidden
+          // by a wolf of this launch that acted before i
+          uint32_t alive = 0xFFFFFFFFu;
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) pp[kk] = *reinterpret_cast<const uint2*>(posw + 4 * kk + 2 * hf);
+          for (int k = 0; k < kOMax; ++k)
+            if (k < NO) {
+              const uint32_t okb = s.ost[k * kWorlds + w];
+              const int h = s.hid[k * kWorlds + w];
+              if (!ost_visible(okb) || h < i) alive &= ~(1u << k);
+            }
+          // rows of the frame: alive (the ostriches) and existing (j < N)
+          const uint32_t vmask = alive & exist & (!bush && (WAB2_ABLATE & 1) ? 0u : ~0u);
+          // entity j is where observer i sees it: after its act if it acted in this launch
+          // before i (a0 <= j < i), else at its frame position from before the launch
+          const int jn = min(i, a1);
+          uint32_t vis = 0, d[NKK];
+          uint2 pp[NKK];  // this lane's entities of the world, all loads issued before any use
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) pp[kk] = *reinterpret_cast<const uint2*>(posw + 4 * kk + 2 * hf);
+          if (bush) {
+            // radius 0: the entities on the observer's tile (its frame X/Y before its act)
+            const uint32_t tgt = pi & 0xFFFFu;
+#pragma unroll
+            for (int kk = 0; kk < NKK; ++kk) {
+              const int j = 4 * kk + 2 * hf;
+              const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
+              const uint32_t e0 = (uint32_t)(((pp[kk].x >> s0) & 0xFFFFu) == tgt);
+              const uint32_t e1 = (uint32_t)(((pp[kk].y >> s1) & 0xFFFFu) == tgt);
+              vis |= ((vmask >> j) & (e0 | (e1 << 1))) << j;
+              d[kk] = 0u;
+            }
+          } else {
+            View v;
+            v.ex = (int)(pi & 0xFFu);
+            v.ey = (int)((pi >> 8) & 0xFFu);
+            v.W = W;
+            v.H = H;
+            // World.get_observations (:365-374)
+            const int r = type == T_OSTRICH ? (role == 1 ? p.rg : p.rl) : p.rw;
+            const int rc = min(r, 255);
+            v.r2 = rc * rc;  // (dx^2 + dy^2) ** 0.5 <= r  <=>  dx^2 + dy^2 <= r^2 (integers)
+            v.xl = v.ex < r ? max(W - r + v.ex, v.ex + W / 2 + 1) : 0x7FFF;
+            v.xr = (v.ex >= r && W < v.ex + r) ? min(r - W + v.ex, v.ex - W / 2 - 1) : -0x7FFF;
+            v.yl = v.ey < r ? max(H - r + v.ey, v.ey + H / 2 + 1) : 0x7FFF;
+            v.yr = (v.ey >= r && H < v.ey + r) ? min(r - H + v.ey, v.ey - H / 2 - 1) : -0x7FFF;
+            v.alive = alive;
 #if WAB2_PACKED
-        View2 v2;
-        v2.e = (s16x2){(short)v.ex, (short)v.ey};
-        v2.lo = (s16x2){(short)min(v.xl, 0x4000), (short)min(v.yl, 0x4000)};
-        v2.hi = (s16x2){(short)max(v.xr, -0x4000), (short)max(v.yr, -0x4000)};
-        v2.wh = (s16x2){(short)W, (short)H};
-        v2.r2 = v.r2;
-        // rows of the frame: alive (the ostriches) and existing (j < N)
-        const uint32_t vmask = v.alive & (N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u) & (WAB2_ABLATE & 1 ? 0u : ~0u);
+            View2 v2;
+            v2.e = (s16x2){(short)v.ex, (short)v.ey};
+            v2.lo = (s16x2){(short)min(v.xl, 0x4000), (short)min(v.yl, 0x4000)};
+            v2.hi = (s16x2){(short)max(v.xr, -0x4000), (short)max(v.yr, -0x4000)};
+            v2.wh = (s16x2){(short)W, (short)H};
+            v2.r2 = v.r2;
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) {
-          const int j = 4 * kk + 2 * hf;
-          const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
-          uint32_t ok0, ok1;
-          const uint32_t p0 = view_pair2(v2, (pp[kk].x >> s0) & 0xFFFFu, ok0);
-          const uint32_t p1 = view_pair2(v2, (pp[kk].y >> s1) & 0xFFFFu, ok1);
-          const uint32_t m = (vmask >> j) & (ok0 | (ok1 << 1));
-          vis |= m << j;
-          d[kk] = (p0 & (0u - (m & 1u))) | ((p1 << 16) & (0u - (m >> 1)));
-        }
+            for (int kk = 0; kk < NKK; ++kk) {
+              const int j = 4 * kk + 2 * hf;
+              const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
+              uint32_t ok0, ok1;
+              const uint32_t p0 = view_pair2(v2, (pp[kk].x >> s0) & 0xFFFFu, ok0);
+              const uint32_t p1 = view_pair2(v2, (pp[kk].y >> s1) & 0xFFFFu, ok1);
+              const uint32_t m = (vmask >> j) & (ok0 | (ok1 << 1));
+              vis |= m << j;
+              d[kk] = (p0 & (0u - (m & 1u))) | ((p1 << 16) & (0u - (m >> 1)));
+            }
 #else
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) {
-          const int j = 4 * kk + 2 * hf;
-          // 16-bit shift by 16 where the entity acted before i in this launch (a0 <= j < i)
-          const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
-          const uint32_t x0 = (pp[kk].x >> s0) & 0xFFFFu, x1 = (pp[kk].y >> s1) & 0xFFFFu;
-          d[kk] = view_pair(v, x0, j, (uint32_t)(j < N) & (uint32_t)!(WAB2_ABLATE & 1), vis) |
-                  (view_pair(v, x1, j + 1, (uint32_t)(j + 1 < N) & (uint32_t)!(WAB2_ABLATE & 1), vis) << 16);
-        }
+            for (int kk = 0; kk < NKK; ++kk) {
+              const int j = 4 * kk + 2 * hf;
+              // 16-bit shift by 16 where the entity acted before i in this launch (a0 <= j < i)
+              const uint32_t s0 = (uint32_t)((j >= a0) & (j < jn)) << 4, s1 = (uint32_t)((j + 1 >= a0) & (j + 1 < jn)) << 4;
+              const uint32_t x0 = (pp[kk].x >> s0) & 0xFFFFu, x1 = (pp[kk].y >> s1) & 0xFFFFu;
+              d[kk] = view_pair(v, x0, j, (vmask >> j) & 1u, vis) | (view_pair(v, x1, j + 1, (vmask >> (j + 1)) & 1u, vis) << 16);
+            }
 #endif
-        vis |= __shfl_xor(vis, 32);
-        // internal obs (World.py:17-18, 50-51, 80-81)
-        double food;
-        int x, y;
-        if (type == T_BUSH) {
-          const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
-          x = (int)(bxy & 0xFFu);
-          y = (int)(bxy >> 8);
-          food = (double)s.bf1[w * NBp + i - NM];  // the bushes act after every ostrich
-        } else {
-          const int2 xy = s.oxy[i * kWorlds + w];
-          x = xy.x;
-          y = xy.y;
-          food = s.food[i * kWorlds + w];
-        }
-        const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
-        if (whole_turn && on && hf == 0) {
-          float rew;
-          uint8_t dn;
-          reward_done(type, status, type == T_WOLF && s.gain[i * kWorlds + w] ? food + p.wff : food, rew, dn);
-          p.reward[(int64_t)t * p.B * N + item0 + q] = rew;
-          p.done[(int64_t)t * p.B * N + item0 + q] = dn;
-        }
-        uint8_t* rec = stage + (lane & 31) * R;
-        if (hf == 0) {
-          const uint64_t fb = (uint64_t)__double_as_longlong(food);
-          *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
-          *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
-        } else {
-          for (int z = 24 + 4 * nd; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
-        }
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk)
-          if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
-        // Additional_Data [food] of the visible bushes as the observer sees them: after the
-        // eats of the ostriches that acted before it in this launch (bf1 for every observer
-        // after the ostriches); byte pairs m = 2mm + half
-        for (int m = hf; m < ((WAB2_ABLATE & 4) ? 0 : nbp); m += 2) {
-          const int b = 2 * m;
-          const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
-          uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
-          if (type == T_OSTRICH) {
-            for (int k = a0; k < min(a1, NO); ++k)
-              if (k < i) {
-                const uint32_t e = s.ev[k * kWorlds + w];
-                if ((e & 0xFFu) == (uint32_t)b) f = (f & 0xFF00u) | (e >> 8);
-                if ((e & 0xFFu) == (uint32_t)b + 1u) f = (f & 0x00FFu) | (e & 0xFF00u);
-              }
           }
-          const uint32_t vb = vis >> (NM + b);
-          f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
-          *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
+          vis |= __shfl_xor(vis, 32);
+          // internal obs (World.py:17-18, 50-51, 80-81)
+          double food;
+          int x, y;
+          if (bush) {
+            const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
+            x = (int)(bxy & 0xFFu);
+            y = (int)(bxy >> 8);
+            food = (double)s.bf1[w * NBp + i - NM];  // the bushes act after every ostrich
+          } else {
+            const int2 xy = s.oxy[i * kWorlds + w];
+            x = xy.x;
+            y = xy.y;
+            food = s.food[i * kWorlds + w];
+          }
+          const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
+          if (whole_turn && on && hf == 0) {
+            float rew;
+            uint8_t dn;
+            reward_done(type, status, type == T_WOLF && s.gain[i * kWorlds + w] ? food + p.wff : food, rew, dn);
+            const int64_t o = (int64_t)t * p.B * N + (wg0 + w) * N + i;
+            p.reward[o] = rew;
+            p.done[o] = dn;
+          }
+          uint8_t* rec = stage + (lane & 31) * R;
+          if (hf == 0) {
+            const uint64_t fb = (uint64_t)__double_as_longlong(food);
+            *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
+            *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
+          } else {
+            for (int z = 24 + 4 * nd; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
+          }
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk)
+            if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+          // Additional_Data [food] of the visible bushes as the observer sees them: after the
+          // eats of the ostriches that acted before it in this launch (bf1 for every observer
+          // after the ostriches); byte pairs m = 2mm + half
+          for (int m = hf; m < ((WAB2_ABLATE & 4) ? 0 : nbp); m += 2) {
+            const int b = 2 * m;
+            const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
+            uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
+            if (!bush && type == T_OSTRICH) {
+              for (int k = a0; k < min(a1, NO); ++k)
+                if (k < i) {
+                  const uint32_t e = s.ev[k * kWorlds + w];
+                  if ((e & 0xFFu) == (uint32_t)b) f = (f & 0xFF00u) | (e >> 8);
+                  if ((e & 0xFFu) == (uint32_t)b + 1u) f = (f & 0x00FFu) | (e & 0xFF00u);
+                }
+            }
+            const uint32_t vb = vis >> (NM + b);
+            f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
+            *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          // the round's records: runs of consecutive records in HBM (a world's observers of this
+          // class), 16 bytes per lane, consecutive lanes at consecutive addresses within a run
+          const int q0 = rnd * 32;
+          const int chunks = min(32, nitems - q0) * CR;
+          for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
+            const int r = (int)(((uint32_t)c * p.magic_cr) >> 16);  // stage slot: c / CR
+            const int qq = q0 + r;
+            const int ww = (int)(((uint32_t)qq * magic) >> 20);
+            const int64_t recno = item0 + ww * no + (c0 - o0) + (qq - ww * nc);
+            const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
+            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(obs_t + recno * R + 16 * (c - r * CR)));
+          }
+          __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the round's records are contiguous in HBM: 16 bytes per lane, 1 KiB per instruction
-        const int q0 = rnd * 32;
-        const int cnt = min(32, nitems - q0);
-        const int chunks = cnt * R / 16;
-        uint8_t* dst = obs_t + (item0 + q0) * (int64_t)R;
-        for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-          const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
-          __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(dst + 16 * c));
-        }
-        __builtin_amdgcn_wave_barrier();
       }
     }
     lds_barrier();
@@ -876,8 +910,14 @@ const void* torus_kernel(int N) {
   }
 }
 
-void launch_torus(const wab2_handle* h, const TParams& p, hipStream_t stream) {
+uint32_t magic20(int n) { return n > 0 ? (uint32_t)(((1u << 20) + (uint32_t)n - 1u) / (uint32_t)n) : 0u; }
+
+void launch_torus(const wab2_handle* h, const TParams& p0, hipStream_t stream) {
   const dim3 grid((unsigned)h->n_blocks), block(wab2::kThreads);
+  TParams p = p0;
+  p.magic_m = magic20(std::min(p.o1, p.NM) - p.o0);
+  p.magic_b = magic20(p.o1 - std::max(p.o0, p.NM));
+  p.magic_cr = (uint32_t)((65536 + p.R / 16 - 1) / (p.R / 16));
   switch ((p.N + 3) / 4) {
     case 1: hipLaunchKernelGGL(wab2::wab_torus_kernel<1>, grid, block, h->lds, stream, p); break;
     case 2: hipLaunchKernelGGL(wab2::wab_torus_kernel<2>, grid, block, h->lds, stream, p); break;
@@ -934,7 +974,6 @@ int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t wo
   p.autoreset = cfg->autoreset ? 1 : 0;
   p.a0 = p.o0 = 0;
   p.a1 = p.o1 = p.N;
-  p.magic_o = (uint32_t)(((1u << 20) + (uint32_t)p.N - 1u) / (uint32_t)p.N);
   p.B = batch;
   h->n_blocks = (int)((batch + wab2::kWorlds - 1) / wab2::kWorlds);
   p.Bp = (int64_t)h->n_blocks * wab2::kWorlds;
@@ -1045,7 +1084,6 @@ int wab2_get_obs(wab2_handle* h, int32_t entity, uint8_t* obs, void* stream) {
   p.a0 = p.a1 = entity;  // nothing acts
   p.o0 = entity;
   p.o1 = entity + 1;
-  p.magic_o = 1u << 20;
   p.obs = obs;
   p.actions = nullptr;
   p.reward = nullptr;
