@@ -1099,7 +1099,8 @@ def main():
         achieved = achieved_rank
         value = world * B * K / elapsed
         # the committed PMC traffic is of the default launch of each config (C5: the fused one)
-        tkey = args.config + ("_rollout%d" % T_roll if rollout or c5_roll else "")
+        tkey = args.config + ("_rollout%d" % T_roll if rollout or c5_roll else
+                              "_ring%d" % args.obs_ring if args.obs_ring else "")
         traffic, traffic_src = committed_traffic(tkey, B) if not args.c5_unfused else (None, None)
         line = {
             "metric": METRIC,
