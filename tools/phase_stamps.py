@@ -269,9 +269,26 @@ def rollout_wide_report(env, st, g, launches, T):
         xcc = s[:, 33]
         acc.setdefault("xcd", []).append([(ex - ent)[xcc == x].mean() if (xcc == x).any() else 0.0 for x in range(8)])
         acc.setdefault("quart", []).append([q.mean() for q in np.array_split(ex - ent, 8)])
-        acc.setdefault("cores", []).append(coresidency(s, ent, ex))
+        co = coresidency(s, ent, ex)
+        acc.setdefault("cores", []).append(co)
         acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean(), np.percentile(ent - ent.min(), 99),
                                              np.percentile(ex - ent.min(), 1), np.percentile(ex - ent.min(), 50)))
+        # the middle step's stamps by dispatch rank on the CU (0..3)
+        rk = co[5]
+        for k, cols in seqs.items():
+            v = s[:, cols]
+            ok = (v > 0).all(axis=1)
+            acc.setdefault("rank_" + k, []).append(
+                [(v[ok & (rk == r)] - t0[ok & (rk == r), None]).mean(axis=0) if (ok & (rk == r)).any()
+                 else np.zeros(len(cols)) for r in range(4)])
+        acc.setdefault("rank_end", []).append([(s[rk == r, 38] - t0[rk == r]).mean() if (rk == r).any() else 0.0
+                                               for r in range(4)])
+    for k in seqs:
+        a = np.mean(acc["rank_" + k], axis=0) * 10 / 1000
+        for r in range(4):
+            print("  rank %d %s: %s" % (r, k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a[r]))))
+    print("  middle step: step start -> past its end barrier by rank: %s us"
+          % np.round(np.mean(acc["rank_end"], axis=0) * 10 / 1000, 2))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
@@ -296,15 +313,17 @@ def coresidency(s, ent, ex):
     key = (s[:, 33] << 8) | ((hw[:, 0] >> 8) & 0xFF)
     dur = ex - ent
     by_rank, by_share = [[] for _ in range(8)], [[] for _ in range(4)]
+    rank = np.full(len(ent), -1)
     for k in np.unique(key):
         idx = np.nonzero(key == k)[0]
         idx = idx[np.argsort(ent[idx], kind="stable")]
         for r, i in enumerate(idx[:8]):
             by_rank[r].append(dur[i])
+            rank[i] = r
             by_share[min(3, int((simd[idx, 0] == simd[i, 0]).sum()) - 1)].append(dur[i])
     offs = np.bincount(((simd[:, 1:] - simd[:, :1]) % 4).ravel(), minlength=4)
     return ([np.mean(v) if v else 0.0 for v in by_rank], [np.mean(v) if v else 0.0 for v in by_share],
-            [len(v) for v in by_share], offs, np.bincount(np.bincount(np.unique(key, return_inverse=True)[1])))
+            [len(v) for v in by_share], offs, np.bincount(np.bincount(np.unique(key, return_inverse=True)[1])), rank)
 
 
 def print_coresidency(rows):
@@ -358,9 +377,26 @@ def rollout_report(env, st, g, launches, T, features=False):
         ent, ex, xcc = s[:, 32], s[:, 39], s[:, 33]
         acc.setdefault("xcd", []).append([(ex - ent)[xcc == x].mean() if (xcc == x).any() else 0.0 for x in range(8)])
         acc.setdefault("eighth", []).append([q.mean() for q in np.array_split(ex - ent, 8)])
-        acc.setdefault("cores", []).append(coresidency(s, ent, ex))
+        co = coresidency(s, ent, ex)
+        acc.setdefault("cores", []).append(co)
         acc.setdefault("launch", []).append((ex.max() - ent.min(), (ex - ent).mean(), np.percentile(ent - ent.min(), 99),
                                              np.percentile(ex - ent.min(), 1), np.percentile(ex - ent.min(), 50)))
+        # the middle step's stamps by dispatch rank on the CU (0..3)
+        rk = co[5]
+        for k, cols in seqs.items():
+            v = s[:, cols]
+            ok = (v > 0).all(axis=1)
+            acc.setdefault("rank_" + k, []).append(
+                [(v[ok & (rk == r)] - t0[ok & (rk == r), None]).mean(axis=0) if (ok & (rk == r)).any()
+                 else np.zeros(len(cols)) for r in range(4)])
+        acc.setdefault("rank_end", []).append([(s[rk == r, 38] - t0[rk == r]).mean() if (rk == r).any() else 0.0
+                                               for r in range(4)])
+    for k in seqs:
+        a = np.mean(acc["rank_" + k], axis=0) * 10 / 1000
+        for r in range(4):
+            print("  rank %d %s: %s" % (r, k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a[r]))))
+    print("  middle step: step start -> past its end barrier by rank: %s us"
+          % np.round(np.mean(acc["rank_end"], axis=0) * 10 / 1000, 2))
     for k in seqs:
         a = np.mean(acc[k], axis=0) * 10 / 1000
         print("%s: %s" % (k, ", ".join("%s %.2f" % (n, v) for n, v in zip(names[k], a))))
