@@ -16,6 +16,12 @@ def _env(opts=None, n=4096, base=0, **kw):
     return BatchedWolvesAndBushesEnv(opts, num_envs=n, seed=SEED, device="cuda:0", env_id_base=base, **kw)
 
 
+def _device_counters(env):
+    """env.counters() without the host-side launch tallies (which differ by design between a
+    rollout handle and a step-loop handle)."""
+    return {k: v for k, v in env.counters().items() if k not in ("rollout_launches", "rollout_step_calls")}
+
+
 def _oracle(opts=None, n=4096, base=0, autoreset=True, stride=0):
     from oracle.oracle import OracleBatch
 
@@ -404,7 +410,7 @@ def test_rollout_variants_equal_step_loop(opts, kw):
     s1, s2 = e1.state(), e2.state()
     for k in s1:
         assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
 
 
 def test_full_size_properties():
@@ -586,7 +592,7 @@ def test_step_features_full_size_c5():
         assert bool((fa[:, o:o + n].sum(1) == 1).all()), o
         o += n
     assert bool((fa[:, o:] == 0).all())  # view mask: zeros without restrict_view
-    assert ea.counters() == eb.counters()
+    assert _device_counters(ea) == _device_counters(eb)
 
 
 def test_step_features_argument_errors():
@@ -835,7 +841,7 @@ def test_rollout_features_equals_step_features_loop(opts, kw, T, planes):
     s1, s2 = e1.state(), e2.state()
     for k in s1:
         assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
 
 
 def test_rollout_features_full_size_c5():
@@ -878,7 +884,7 @@ def test_rollout_features_full_size_c5():
                 R = 0.0
             R = exact.get(np.float32(rt[t, b]), float(rt[t, b])) + 0.99 * R
             assert np.float32(R) == ret[t, b], (b, t)
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
 
 
 # ------------------------------------------------------------------ the wide kernel's rollout build
@@ -924,7 +930,7 @@ def test_wide_rollout_equals_step_loop(opts, stride, slots, autoreset):
     s1, s2 = e1.state(), e2.state()
     for k in s1:
         assert np.array_equal(np.asarray(s1[k]), np.asarray(s2[k])), k
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
 
 
 @pytest.mark.parametrize("wide", [False, True])
@@ -943,7 +949,7 @@ def test_rollout_tiny_batch(wide):
         e2.step(a[t])
         assert torch.equal(planes[t], e2._obs["planes"]), t
         assert torch.equal(rew[t], e2.reward), t
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
 
 
 def test_wide_rollout_full_size_c3():
@@ -970,7 +976,7 @@ def test_wide_rollout_full_size_c3():
             assert torch.equal(rew[t], e2.reward) and torch.equal(done[t].bool(), e2.done.bool()), (seg, t)
             assert torch.equal(scal[t], e2._obs["scalars"]), (seg, t)
         del planes
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
 
 
 @pytest.mark.parametrize("wide", [False, True])
@@ -996,7 +1002,7 @@ def test_rollout_short_segments(wide, T):
             e2.step(a[t])
             assert torch.equal(planes[t], e2._obs["planes"]), (seg, t)
             assert torch.equal(rew[t], e2.reward) and torch.equal(done[t].bool(), e2.done.bool()), (seg, t)
-    assert e1.counters() == e2.counters()
+    assert _device_counters(e1) == _device_counters(e2)
     if not wide:
         e3, e4 = _env(None, B, **kw), _env(None, B, **kw)
         e3.reset()
@@ -1026,6 +1032,7 @@ def test_env_buffers_after_rollouts():
     planes, scal, rew, done = e1.rollout(a)
     for t in range(T):
         e2.step(a[t])
+    e1._require_planes()  # (the env's own planes are copied from planes[T-1] when first needed)
     assert torch.equal(e1._obs["planes"], e2._obs["planes"]) and torch.equal(e1._obs["planes"], planes[-1])
     assert torch.equal(e1._obs["scalars"], e2._obs["scalars"])
     assert torch.equal(e1.reward, e2.reward) and torch.equal(e1.done, e2.done)

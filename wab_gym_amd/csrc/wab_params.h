@@ -171,7 +171,13 @@ struct SmallLayout {
   uint32_t stream2;     // multi-step launches: the second obs bit-stream (steps alternate)
   uint32_t fbits, fzero, ftab, scal, total;  // fused features (wab_step_features): bits, tables, scalars
   uint32_t rcode;       // wab_rollout_features with returns: [n_steps][64] reward codes (bytes)
+  uint32_t wcar;        // multi-step launches of 32-slot handles: W2's wolf slots between steps ([k][64])
 };
+
+// wolf slots a multi-step launch carries in W2's registers from step to step: all of them up to
+// 16 slots; a 32-slot handle carries its slots in LDS (Lds::wcar), so that the carry and the
+// step's own 32 slots do not overflow the 128 VGPRs (132 bytes per lane of scratch otherwise)
+__host__ __device__ constexpr int carry_reg_slots(int slots) { return slots <= 16 ? slots : 0; }
 
 __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   // (the regions whose size depends on a runtime option come last, so that with the G = 11
@@ -196,6 +202,8 @@ __host__ __device__ inline SmallLayout small_layout(const Params& p) {
   L.act = o; o += 16u;         // 64 int8 actions
   L.elog = o; o += (uint32_t)(kSmallLog - 4) * 64u * 5u / 4u;
   L.stream2 = o; o += L.stream_words + 4u;
+  L.wcar = o;
+  if (p.wolf_cap > 16) o += (uint32_t)(p.wolf_cap - carry_reg_slots(p.wolf_cap)) * 64u;
   L.gap = o; o += lds_align4(2u * ((uint32_t)p.n_gap + 1u));          // spawn-set gap table
   L.thr = o; o += lds_align4(2u * ((uint32_t)p.max_berries + 4u));  // pad, T_1..T_n, 2 pads
   L.fbits = L.ftab = L.fzero = L.scal = o;

@@ -276,6 +276,7 @@ struct Lds {
   uint32_t* carry;  // [64][8] multi-step launches: a new episode's role | wolves << 8, food, wolf cells (W3)
   uint32_t* act;    // [16] multi-step launches: the next step's 64 actions (W1)
   uint8_t* rcode;   // [n_steps][64] wab_rollout_features with returns: each step's reward code (W0)
+  uint32_t* wcar;   // [slots][64] multi-step launches of 32-slot handles: W2's wolf slots between steps
   uint32_t* elxy;   // [kSmallLog - 4][64] multi-step launches: eaten-log entries 4.. (W0)
   uint8_t* elrem;   // [kSmallLog - 4][64]
 };
@@ -302,6 +303,7 @@ __device__ __forceinline__ Lds lds_of(uint32_t* lds, const SmallLayout& L) {
   s.scal = lds + L.scal;
   s.carry = lds + L.carry;
   s.act = lds + L.act;
+  s.wcar = lds + L.wcar;
   s.rcode = reinterpret_cast<uint8_t*>(lds + L.rcode);
   return s;
 }
@@ -456,10 +458,11 @@ struct CarryW0 {
 };
 template <int SLOTS>
 struct CarryW2 {
+  static constexpr int NR = carry_reg_slots(SLOTS);
   uint8_t* prev_planes;
   uint32_t* prev_stream;
   uint4 hdr;
-  uint32_t wr[SLOTS];  // wolf tiles, uncompacted
+  uint32_t wr[NR > 0 ? NR : 1];  // wolf tiles, uncompacted: slots 0 .. NR-1 (the rest in Lds::wcar)
   uint32_t live;       // occupied slots
 };
 
@@ -1050,8 +1053,9 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   if (carried) {
     hr.hdr = carry->hdr;
     hr.a = act_of(s, lane);
+    constexpr int NR = CarryW2<SLOTS>::NR;
 #pragma unroll
-    for (int k = 0; k < SLOTS; ++k) wr[k] = carry->wr[k];
+    for (int k = 0; k < SLOTS; ++k) wr[k] = k < NR ? carry->wr[k < NR ? k : 0] : s.wcar[(k - NR) * 64 + lane];
   } else {
   {
     const int64_t gl = active ? g : 0;  // (unconditional; an inactive lane has no live wolf)
@@ -1190,19 +1194,26 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
     if (job) {
       const NewEp n = carry_of(s, lane);
       M128 m = n.wolves;
+      constexpr int NR = CarryW2<SLOTS>::NR;
 #pragma unroll
       for (int k = 0; k < SLOTS; ++k) {
         const bool any = (m.lo | m.hi) != 0ull;
         const uint32_t c = m.lo ? (uint32_t)(__ffsll((unsigned long long)m.lo) - 1)
                                 : (uint32_t)(__ffsll((unsigned long long)m.hi) + 63);
-        carry->wr[k] = any ? s.tiles[any ? c : 0u] : 0u;
+        const uint32_t w = any ? s.tiles[any ? c : 0u] : 0u;
+        if (k < NR) carry->wr[k < NR ? k : 0] = w;
+        else s.wcar[(k - NR) * 64 + lane] = w;
         if (any) m_clear(m, c);
       }
       carry->live = n.nw >= 32u ? ~0u : ((1u << n.nw) - 1u);
       carry->hdr = new_header(n, h);
     } else {
+      constexpr int NR = CarryW2<SLOTS>::NR;
 #pragma unroll
-      for (int k = 0; k < SLOTS; ++k) carry->wr[k] = wr[k];
+      for (int k = 0; k < SLOTS; ++k) {
+        if (k < NR) carry->wr[k < NR ? k : 0] = wr[k];
+        else s.wcar[(k - NR) * 64 + lane] = wr[k];
+      }
       carry->live = live;
       const uint32_t status = starved ? 1u : kill ? 2u : misc_status(h.hdr.z);
       carry->hdr = make_uint4(h.cpos, (uint32_t)h.turn,
