@@ -106,6 +106,54 @@ __device__ __forceinline__ void plane_features(const FeatTables& t, int md, M128
   second = n2 >= 0 ? t.enc[n2] : 0u;
 }
 
+// the split of plane_features over waves (the fused rollout): the capped direction counts alone
+__device__ __forceinline__ void plane_counts(const FeatTables& t, const M128& P, int counts[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) counts[k] = min(m_popc(m_and(P, m_of(t.cmask[k]))), 10);
+}
+
+// ... and nearest / second nearest alone
+__device__ __forceinline__ void plane_nearest(const FeatTables& t, int md, M128 P, uint32_t& near, uint32_t& second) {
+  int n1 = -1, n2 = -1;
+  for (int d = 0; d < md; ++d) {
+    if (__all(n2 >= 0 || (P.lo | P.hi) == 0ull)) break;  // (wave-uniform exit)
+    const M128 r = m_of(t.ring[d]);
+    M128 m = m_and(P, r);
+    P = m_andn(P, r);
+    const int top = m_top(m);
+    if (n1 < 0) {
+      if (top >= 0) {
+        n1 = top;
+        m_clear(m, (uint32_t)top);
+        n2 = m_top(m);
+      }
+    } else if (n2 < 0) {
+      n2 = top;
+    }
+  }
+  near = n1 >= 0 ? t.enc[n1] : 0u;
+  second = n2 >= 0 ? t.enc[n2] : 0u;
+}
+
+// emit_plane's parts: the 8 nearest / second-nearest features, the 4 count features
+__device__ __forceinline__ void emit_nearest(uint32_t* ob, uint32_t at, int plane, int md, uint32_t near,
+                                             uint32_t second) {
+  const uint32_t M1 = (uint32_t)md + 1u;
+  const uint32_t base = at + (uint32_t)plane * (8u * M1 + 44u);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fset(ob, base + (uint32_t)k * M1 + ((near >> (8 * k)) & 0xFFu));
+    fset(ob, base + (4u + (uint32_t)k) * M1 + ((second >> (8 * k)) & 0xFFu));
+  }
+}
+
+__device__ __forceinline__ void emit_counts(uint32_t* ob, uint32_t at, int plane, int md, const int counts[4]) {
+  const uint32_t M1 = (uint32_t)md + 1u;
+  const uint32_t base = at + (uint32_t)plane * (8u * M1 + 44u);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fset(ob, base + 8u * M1 + 11u * (uint32_t)k + (uint32_t)counts[k]);
+}
+
 // one plane's 12 one-hot features (plane 0 wolves, 1 bushes) of the env whose row starts at
 // feature bit `at`
 __device__ __forceinline__ void emit_plane(uint32_t* ob, uint32_t at, int plane, int md, uint32_t near,

@@ -1424,7 +1424,30 @@ __device__ __forceinline__ void step_features(const Params& p, const SmallLayout
   const uint32_t n_active = (uint32_t)min((int64_t)64, p.B - g0);
   const uint32_t* stream = lds + L.stream;
   uint32_t* ob = lds + L.fbits;
-  if ((uint32_t)lane < n_active && wave < 3) {
+  if (ROLL && (uint32_t)lane < n_active) {
+    // multi-step launches: the emit over all four waves (W0, W1 the two planes' nearest cells,
+    // W2 both planes' direction counts, W3 the scalars and view mask)
+    const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, at = (uint32_t)lane * F;
+    const FeatTables ft = feat_tables_at(lds + L.ftab, md);
+    if (wave <= 1) {
+      uint32_t near, second;
+      plane_nearest(ft, md, stream_get128(stream, ebit + (uint32_t)wave * WH, WH), near, second);
+      emit_nearest(ob, at, wave, md, near, second);
+    } else if (wave == 2) {
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        int counts[4];
+        plane_counts(ft, stream_get128(stream, ebit + (uint32_t)pl * WH, WH), counts);
+        emit_counts(ob, at, pl, md, counts);
+      }
+    } else {
+      const uint32_t sc = lds[L.scal + lane];
+      const uint32_t role = (sc >> 8) & 0xFFu;
+      const uint32_t sb_bit = ebit + WH + (uint32_t)(md / 2) * (uint32_t)p.S + (uint32_t)(md / 2);  // :742
+      emit_scalars(ob, at, md, p.turns_empty, (stream[sb_bit >> 5] >> (sb_bit & 31u)) & 1u, sc & 0xFFu, role,
+                   sc >> 16, p.restrict_view != 0, view_mask_of(p, (int)role));
+    }
+  } else if ((uint32_t)lane < n_active && wave < 3) {
     const uint32_t ebit = (uint32_t)lane * (uint32_t)p.OB, at = (uint32_t)lane * F;
     if (wave <= 1) {  // W0 wolves, W1 bushes
       uint32_t near, second;
