@@ -38,7 +38,7 @@
 
 // Diagnostic builds only (tools/ab_torus.sh; results wrong by design): WAB2_ABLATE bit 1 skips
 // the view computation of the records, bit 2 their global stores, bit 4 the bush-food bytes,
-// bit 8 phase C.
+// bit 8 phase C, bit 16 the bush observers' rounds, bit 32 the movers' rounds, bit 64 phase A.
 #ifndef WAB2_ABLATE
 #define WAB2_ABLATE 0
 #endif
@@ -375,7 +375,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   int64_t resets = 0;
   for (int t = 0; t < T; ++t) {
     // ================= phase A: the sequential part of the turn, one lane per world
-    if (wave == 0) {
+    if (WAB2_ABLATE & 64) {
+    } else if (wave == 0) {
       WAB2_PHASE_PARAMS;
       const uint8_t* A = (t & 1) ? s.act1 : s.act0;
       // ostriches in id order: act (World.py:25-43), X = x mod W (:331-332), eat (:118-132)
@@ -518,7 +519,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const int c0 = bush ? max(o0, NM) : o0, c1 = bush ? p.o1 : min(p.o1, NM);
         const int nc = max(0, c1 - c0);
         const uint32_t magic = bush ? p.magic_b : p.magic_m;  // q / nc = (q * magic) >> 20
-        const int nitems = nvalid * nc;
+        const int nitems = (WAB2_ABLATE & (bush ? 16 : 32)) ? 0 : nvalid * nc;
         for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
           const int q = rnd * 32 + (lane & 31);
           const bool on = q < nitems;
