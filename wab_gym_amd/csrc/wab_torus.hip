@@ -136,6 +136,8 @@ struct Lds {
   uint8_t* ost;      // [NO][64] ostrich state byte before the launch
   uint8_t* hid;      // [NO][64] the wolf whose kill hid label k in this launch (0xFF: none)
   uint8_t* killed;   // [NO][64] status set to 2 in this launch
+  uint8_t* alv;      // [NM + 1][64] the ostriches still Visible for observer i (i = NM: every bush):
+                     // bit k, bits >= NO set (W1, phase A)
 };
 
 __host__ __device__ inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -147,7 +149,7 @@ __host__ __device__ inline int bush_row(int NB) { return (NB + 3) & ~3; }
 
 struct LdsLayout {
   size_t food, oxy, stage, act0, act1, pos, turn, ep, ep_reset, omod, bxy, ev, bf0, bf1, gain, ost, hid, killed,
-      total;
+      alv, total;
 };
 
 __host__ __device__ inline LdsLayout lds_layout(int N, int NO, int NM, int NB, int R) {
@@ -171,6 +173,7 @@ __host__ __device__ inline LdsLayout lds_layout(int N, int NO, int NM, int NB, i
   L.ost = o; o += align16((size_t)NO * kWorlds);
   L.hid = o; o += align16((size_t)NO * kWorlds);
   L.killed = o; o += align16((size_t)NO * kWorlds);
+  L.alv = o; o += align16((size_t)(NM + 1) * kWorlds);
   L.total = o;
   return L;
 }
@@ -196,6 +199,7 @@ __device__ __forceinline__ Lds lds_tables(uint8_t* base, const TParams& p) {
   s.ost = base + L.ost;
   s.hid = base + L.hid;
   s.killed = base + L.killed;
+  s.alv = base + L.alv;
   return s;
 }
 
@@ -435,6 +439,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           dead |= (uint32_t)(ost_status(ob) != 0) << k;
         }
       }
+      const uint32_t vis0 = vis;  // (before this launch's kills)
       for (int m = max(a0, NO); m < min(a1, NM); ++m) {
         const uint32_t np = moved(s.omod[m * kWorlds + w], (int)(int8_t)A[w * na + m - a0], W, H);
         reinterpret_cast<uint16_t*>(posw + m)[1] = (uint16_t)np;
@@ -466,6 +471,17 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           s.hid[k * kWorlds + w] = (uint8_t)hid_by[k];
           s.killed[k * kWorlds + w] = (uint8_t)(kills >> k & 1u);
         }
+      // the Visible ostriches each observer sees: visible before the launch, not hidden by a
+      // wolf of this launch that acted before it (hid_by < i); bits >= NO set (not ostriches)
+      {
+        uint32_t seen = vis0 | (0xFFu << NO);
+        for (int i = 0; i <= NM; ++i) {
+          s.alv[i * kWorlds + w] = (uint8_t)seen;
+#pragma unroll
+          for (int k = 0; k < kOMax; ++k)
+            if (k < NO && hid_by[k] == (uint32_t)i) seen &= ~(1u << k);
+        }
+      }
       dead |= kills;
       // the turn ends with this launch when its last entity acts; then the batched surface's
       // autoreset: every ostrich done, or max_turns reached
@@ -512,9 +528,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       const int nbp = (NB + 1) >> 1;      // bush-food byte pairs
       const int CR = R >> 4;              // 16-byte chunks per record
       const uint32_t exist = N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u;
+      // the stage starts zero: the bush rounds (first) then write only their headers and bush
+      // bytes (their deltas are zero); the mover rounds write every byte
+      for (int c = lane; c < 2 * R; c += 64) reinterpret_cast<u32x4*>(stage)[c] = (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
       for (int cls = 0; cls < 2; ++cls) {
-        const bool bush = cls == 1;
+        const bool bush = cls == 0;
         // the class's observers [c0, c1) of the window
         const int c0 = bush ? max(o0, NM) : o0, c1 = bush ? p.o1 : min(p.o1, NM);
         const int nc = max(0, c1 - c0);
@@ -531,16 +550,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const uint32_t pi = posw[i];
           const uint32_t ob = (!bush && type == T_OSTRICH) ? s.ost[i * kWorlds + w] : 0u;
           const int role = ost_role(ob), status = ost_status(ob);
-          // ostriches still Visible when i observes: visible before the launch and not hidden
-          // by a wolf of this launch that acted before i
-          uint32_t alive = 0xFFFFFFFFu;
-#pragma unroll
-          for (int k = 0; k < kOMax; ++k)
-            if (k < NO) {
-              const uint32_t okb = s.ost[k * kWorlds + w];
-              const int h = s.hid[k * kWorlds + w];
-              if (!ost_visible(okb) || h < i) alive &= ~(1u << k);
-            }
+          // ostriches still Visible when i observes (Lds::alv)
+          const uint32_t alive = 0xFFFFFF00u | s.alv[min(i, NM) * kWorlds + w];
           // rows of the frame: alive (the ostriches) and existing (j < N)
           const uint32_t vmask = alive & exist & (!bush && (WAB2_ABLATE & 1) ? 0u : ~0u);
           // entity j is where observer i sees it: after its act if it acted in this launch
@@ -635,12 +646,14 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const uint64_t fb = (uint64_t)__double_as_longlong(food);
             *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
             *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
-          } else {
+          } else if (!bush) {
             for (int z = 24 + 4 * nd; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
           }
+          if (!bush) {  // (a bush's deltas are zero: the stage's, since the turn's first round)
 #pragma unroll
-          for (int kk = 0; kk < NKK; ++kk)
-            if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+            for (int kk = 0; kk < NKK; ++kk)
+              if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+          }
           // Additional_Data [food] of the visible bushes as the observer sees them: after the
           // eats of the ostriches that acted before it in this launch (bf1 for every observer
           // after the ostriches); byte pairs m = 2mm + half
