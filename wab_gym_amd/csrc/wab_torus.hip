@@ -545,7 +545,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
           const int w = (int)(((uint32_t)qc * magic) >> 20);
           const int i = c0 + qc - w * nc;
-          const int type = i < NO ? T_OSTRICH : i < NM ? T_WOLF : T_BUSH;
+          const int type = bush ? T_BUSH : i < NO ? T_OSTRICH : T_WOLF;
           const uint32_t* posw = s.pos + w * Np;
           const uint32_t pi = posw[i];
           const uint32_t ob = (!bush && type == T_OSTRICH) ? s.ost[i * kWorlds + w] : 0u;
@@ -657,7 +657,22 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           // Additional_Data [food] of the visible bushes as the observer sees them: after the
           // eats of the ostriches that acted before it in this launch (bf1 for every observer
           // after the ostriches); byte pairs m = 2mm + half
-          for (int m = hf; m < ((WAB2_ABLATE & 4) ? 0 : nbp); m += 2) {
+          if (bush && !(WAB2_ABLATE & 4)) {
+            // a bush sees bf1; its record's bytes around the bush-food ones are zero (deltas,
+            // tail), so the region goes out as whole dwords from bb & ~3: dword k holds bushes
+            // 4k - sh .. 4k - sh + 3, masked by their visibility bits
+            const uint8_t* row = s.bf1 + w * NBp;
+            const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
+            const uint64_t v64 = (uint64_t)vis << 8;  // (bit NM + b + 8: bush b, b >= -8)
+            for (int k = hf; k < ndw; k += 2) {
+              const int b = 4 * k - sh;
+              uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
+              if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
+              const uint32_t b4 = (uint32_t)(v64 >> (NM + b + 8)) & 0xFu;
+              *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+            }
+          }
+          for (int m = hf; m < ((bush || (WAB2_ABLATE & 4)) ? 0 : nbp); m += 2) {
             const int b = 2 * m;
             const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
             uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
@@ -680,13 +695,15 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           // class), 16 bytes per lane, consecutive lanes at consecutive addresses within a run
           const int q0 = rnd * 32;
           const int chunks = min(32, nitems - q0) * CR;
+          const int w0r = (int)(((uint32_t)q0 * magic) >> 20);  // the round's first world
+          uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;  // its first record
           for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
             const int r = (int)(((uint32_t)c * p.magic_cr) >> 16);  // stage slot: c / CR
             const int qq = q0 + r;
             const int ww = (int)(((uint32_t)qq * magic) >> 20);
-            const int64_t recno = item0 + ww * no + (c0 - o0) + (qq - ww * nc);
+            const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
             const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
-            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(obs_t + recno * R + 16 * (c - r * CR)));
+            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
           }
           __builtin_amdgcn_wave_barrier();
         }
