@@ -900,7 +900,7 @@ def test_rollout_features_full_size_c5():
     ({"width": 31, "height": 15, "wolves_can_move": False, "god_mode": True}, 16, 8, True),
     ({"width": 13, "height": 11, "turns_to_fill_food": 4, "max_turns": 60, "bush_power": 60}, 16, 8, True),
     ({"width": 31, "height": 31}, 32, 16, False),                     # stepping past done
-    # eats nearly every turn, two berries per bush: eaten logs past the 16 kept on chip
+    # eats nearly every turn, two berries per bush: eaten logs past the entries the wide rollout keeps on chip (kWideRollLog)
     ({"width": 31, "height": 31, "bush_power": 1, "max_berries_per_bush": 2, "max_turns": 120}, 32, 16, True),
     ({"width": 25, "height": 25, "bush_power": 1, "max_berries_per_bush": 3}, 32, 8, True),
 ])
