@@ -684,6 +684,10 @@ def main():
                          "[B] buffer rewritten every step (which a 256 MB Infinity Cache can absorb)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stream-shards", type=int, default=2,
+                    help="rollout lines: the batch as this many independent shards (handles of B / S envs, "
+                         "contiguous env ids), each shard's launches on its own HIP stream, so that one "
+                         "shard's launch tail overlaps the other's next launch (1: one handle)")
     ap.add_argument("--no-extra", action="store_true",
                     help="default config: skip the other configs' lines (configs key) timed beside it")
     ap.add_argument("--no-diag", action="store_true",
@@ -747,6 +751,9 @@ def main():
     rollout = args.rollout > 0 and not c5
     T_roll = args.rollout
     B, K, W = args.batch, args.steps, args.warmup
+    S = args.stream_shards if rollout else 1
+    if S < 1 or B % (64 * S):
+        S = 1  # (whole 64-env groups per shard)
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
                                     env_id_base=env_id_base(rank, B),
                                     autoreset=True, validate_actions=False, plane_stride=stride,
@@ -834,19 +841,38 @@ def main():
                                "wab_discounted_returns_exact")
     elif rollout:
         T = args.rollout
-        seq_planes = torch.empty((T, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
-        seq_scal = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
-        seq_rew = torch.empty((T, B), dtype=torch.float32, device=dev)
-        seq_done = torch.empty((T, B), dtype=torch.uint8, device=dev)
-        seq = _lib.WabObs(seq_planes.data_ptr(), seq_scal[0].data_ptr(), seq_scal[1].data_ptr(),
-                          seq_scal[2].data_ptr())
-        seq_addr = ctypes.addressof(seq)
+        # the timed workload: the B envs as S shards of Bs envs (ids contiguous, so the union is the
+        # one-handle batch bit for bit), shard k's T-step launches in order on its own stream
+        Bs = B // S
+        shard_envs = [env] if S == 1 else [
+            BatchedWolvesAndBushesEnv(opts, num_envs=Bs, seed=0x5EED, device=dev,
+                                      env_id_base=env_id_base(rank, B) + k * Bs, autoreset=True,
+                                      validate_actions=False, plane_stride=stride, wolf_slots=slots)
+            for k in range(S)]
+        for e in shard_envs[1 if S == 1 else 0:]:
+            e.reset()
+        # each shard's actions [W + K][Bs] contiguous (the same random draws, shard-major)
+        shard_actions = actions.view(W + K, S, Bs).permute(1, 0, 2).contiguous()
+        shard_bufs = []
+        for k, e in enumerate(shard_envs):
+            pl = torch.empty((T, Bs, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+            sc = torch.empty((3, T, Bs), dtype=torch.uint8, device=dev)
+            rw = torch.empty((T, Bs), dtype=torch.float32, device=dev)
+            dn = torch.empty((T, Bs), dtype=torch.uint8, device=dev)
+            o = _lib.WabObs(pl.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
+            shard_bufs.append((e._h, shard_actions[k].data_ptr(), o, pl, sc, rw, dn))
+        shard_streams = [torch.cuda.Stream(dev) for _ in range(S - 1)]
 
         def run(t0, n, stream):
-            s = ctypes.c_void_p(stream.cuda_stream)
+            subs = [stream] + shard_streams  # (forked from `stream`, joined back at the end)
+            for st in shard_streams:
+                st.wait_stream(stream)
             for t in range(t0, t0 + n, T):
-                _lib.check(L.wab_rollout(h, a0 + t * B, T, seq_addr, seq_rew.data_ptr(), seq_done.data_ptr(), s),
-                           "wab_rollout")
+                for (hk, ak, o, pl, sc, rw, dn), st in zip(shard_bufs, subs):
+                    _lib.check(L.wab_rollout(hk, ak + t * Bs, T, ctypes.addressof(o), rw.data_ptr(), dn.data_ptr(),
+                                             ctypes.c_void_p(st.cuda_stream)), "wab_rollout")
+            for st in shard_streams:
+                stream.wait_stream(st)
     elif args.obs_ring > 0:
         N = args.obs_ring
         ring_planes = torch.empty((N, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
@@ -890,6 +916,9 @@ def main():
         print("bench.py: %d steps captured" % K, file=sys.stderr, flush=True)
         # the capture itself did not execute the steps; rewind state by a fresh reset
         env.reset()
+        if rollout and S > 1:
+            for e in shard_envs:
+                e.reset()
         run(0, W, stream)
         torch.cuda.synchronize(dev)
 
@@ -909,7 +938,15 @@ def main():
     if world > 1:  # every rank times the same number of steps
         reps = int(max_over_ranks(reps))
 
-    c_before = env.counters()  # (synchronises; outside the timed region)
+    timed_envs = shard_envs if rollout else [env]
+
+    def workload_counters():
+        out = {}
+        for e in timed_envs:
+            for k_, v in e.counters().items():
+                out[k_] = out.get(k_, 0) + v
+        return out
+    c_before = workload_counters()  # (synchronises; outside the timed region)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -929,7 +966,7 @@ def main():
         dist.barrier()
     elapsed = max_over_ranks(elapsed_rank)
     K_req, K = K, K * reps  # steps in the graph; steps timed
-    c_after = env.counters()
+    c_after = workload_counters()
     window = {"env_steps": c_after["steps"] - c_before["steps"],
               "resets": c_after["resets"] - c_before["resets"],
               "graph_steps": K_req, "graph_replays": reps,
@@ -1010,7 +1047,22 @@ def main():
         _lib.check(L.wab_set_obs_placement(h, _lib.OBS_SAME_BUFFER), "wab_set_obs_placement")
         psc_ms = per_launch(lambda i, s: L.wab_step(h, a0 + (W + i) * B, obs_addr, rew, done, None, s), n_ps)
         del ring_planes
+        # the same rollout as ONE handle of B envs on one stream (the S = 1 line), for comparison
+        one_ms = float("nan")
+        if S > 1 and not args.no_diag:
+            seq_planes = torch.empty((T, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+            seq_scal = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
+            seq_rd = torch.empty((T, B, 5), dtype=torch.uint8, device=dev)
+            seq = _lib.WabObs(seq_planes.data_ptr(), seq_scal[0].data_ptr(), seq_scal[1].data_ptr(),
+                              seq_scal[2].data_ptr())
+            n_one = max(1, min(K_req // T, MIN_TIMED_LAUNCHES))
+            one_ms = per_launch(lambda i, s: L.wab_rollout(h, a0 + (W + (i * T) % K_req) * B, T, ctypes.addressof(seq),
+                                                           seq_rd.data_ptr(), seq_rd.data_ptr() + 4 * T * B, s),
+                                n_one) / T
+            del seq_planes
         roll_line = {"steps_per_launch": T_roll, "launch_us": round(kern_ms * T_roll * 1e3, 3),
+                     "stream_shards": S, "envs_per_launch": B // S,
+                     "one_handle_us_per_step": None if one_ms != one_ms else round(one_ms * 1e3, 3),
                      "per_step_launch": {"api": "wab_step (the raw C-ABI per-step launch), step t's obs into "
                                                 "slot t %% %d of a ring of [B] buffers" % NR,
                                          "us_per_step": round(ps_ms * 1e3, 3),
@@ -1084,7 +1136,7 @@ def main():
                 kernel_name, alg, kern_ms = fk + " (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
             else:
                 kern_ms = step_ms
-    counters = env.counters()
+    counters = workload_counters() if rollout else env.counters()
     achieved_rank = alg * B / (kern_ms * 1e-3) / 1e9
     per_rank = all_gather_objects({
         "rank": rank, "device": str(dev), "pci": pci_id(dev), "env_steps_per_s": round(B * K / elapsed_rank, 1),
@@ -1100,7 +1152,7 @@ def main():
         value = world * B * K / elapsed
         # the committed PMC traffic is of the default launch of each config (C5: the fused one)
         tkey = args.config + ("_rollout%d" % T_roll if rollout or c5_roll else
-                              "_ring%d" % args.obs_ring if args.obs_ring else "")
+                              "_ring%d" % args.obs_ring if args.obs_ring else "") + ("_s%d" % S if S > 1 else "")
         traffic, traffic_src = committed_traffic(tkey, B) if not args.c5_unfused else (None, None)
         line = {
             "metric": METRIC,
@@ -1117,7 +1169,10 @@ def main():
             "dtype": "u8",
             "data": "synthetic: uniform random actions (torch.randint on device), keyed-RNG worlds",
             "config": {"workload": desc + ("; %d-step wab_rollout launches (obs, reward, done of every "
-                                           "step into a [%d, B] rollout buffer)" % (T_roll, T_roll)
+                                           "step into a [%d, B] rollout buffer)%s" % (
+                                               T_roll, T_roll,
+                                               ", the batch as %d shards of %d envs, each on its own HIP stream"
+                                               % (S, B // S) if S > 1 else "")
                                            if rollout else
                                            "; %d-step wab_rollout_features launches (features, reward, done, "
                                            "returns into [%d, B] rollout buffers)" % (T_roll, T_roll)
@@ -1126,13 +1181,14 @@ def main():
                                            if args.obs_ring > 0 else "; one step launch per step"),
                        "batch_per_gpu": B, "global_batch": B * world,
                        "viewport": [Wv, Hv], "plane_stride": env.S, "wolf_slots": slots, "launch": args.mode,
+                       "stream_shards": S,
                        "parallelism": "independent env shards x%d (no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": round(alg * B * (T_roll if rollout or c5_roll else 1)),
+                         "alg_bytes_per_launch": round(alg * (B // S) * (T_roll if rollout or c5_roll else 1)),
                          "kernel": kernel_name,
                          "kernel_us": round(kern_ms * 1e3 * (T_roll if rollout or c5_roll else 1), 3),
                          "alg_bytes_per_env_step": round(alg, 3)},

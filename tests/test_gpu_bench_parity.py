@@ -134,3 +134,47 @@ def test_rollout_features_bench_config_vs_oracle():
         _state_equal(env, orc, "after launch %d" % k)
     c = _counters_clean(env, 4 * T * B)
     assert c["resets"] > 4 * B
+
+
+def test_headline_stream_shards_equal_one_handle():
+    """The headline line as bench.py runs it (--stream-shards 2): the batch as two handles of
+    B / 2 envs (ids 0.. and B/2..), each shard's 64-step launches on its own HIP stream, running
+    concurrently.  Every step's obs, scalars, reward and done, and the final hidden state, equal
+    one handle of B envs stepped with the same actions (which the test above pins to the oracle)."""
+    import torch
+
+    from wab_gym_amd.env import BatchedWolvesAndBushesEnv
+
+    S, Bs = 2, B // 2
+    mk = lambda n, base: BatchedWolvesAndBushesEnv(None, num_envs=n, seed=SEED, device="cuda:0",  # noqa: E731
+                                                   env_id_base=base, autoreset=True, validate_actions=False,
+                                                   wolf_slots=8)
+    one = mk(B, 0)
+    shards = [mk(Bs, k * Bs) for k in range(S)]
+    for e in [one] + shards:
+        e.reset()
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    for k in range(3):  # three launches: past the turn-80 cap of the first episodes
+        a = _actions(900 + k, one.n_actions)
+        a_sh = [a[:, j * Bs:(j + 1) * Bs].contiguous() for j in range(S)]
+        cur = torch.cuda.current_stream()
+        outs = []
+        for j, (e, st) in enumerate(zip(shards, streams)):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                outs.append(e.rollout(a_sh[j]))
+        planes, scal, rew, done = one.rollout(a)
+        for st in streams:
+            cur.wait_stream(st)
+        torch.cuda.synchronize()
+        for j, (p_, s_, r_, d_) in enumerate(outs):
+            sl = slice(j * Bs, (j + 1) * Bs)
+            assert torch.equal(p_, planes[:, sl]), (k, j, "planes")
+            assert torch.equal(s_, scal[:, :, sl]), (k, j, "scalars")
+            assert torch.equal(r_, rew[:, sl]) and torch.equal(d_, done[:, sl]), (k, j, "reward/done")
+        del outs, planes
+    so = one.state()
+    for j, e in enumerate(shards):
+        ss = e.state()
+        for key in ss:
+            assert np.array_equal(ss[key], so[key][j * Bs:(j + 1) * Bs]), (j, key)
