@@ -159,16 +159,30 @@ def torus_actions(T, B, NO, NW, NB, dev, gen):
     return out
 
 
-def time_launches(launch, n, dev, stream, mode="graph", min_seconds=MIN_TIMED_SECONDS):
-    """Average duration of one of `n` back-to-back launches (launch(i, hip_stream)), captured in a
-    graph as the timed region is, replayed until at least `min_seconds` are timed; HIP events on
-    the launch stream.  Returns (ms per launch, launches timed)."""
+def time_launches(launch, n, dev, stream, mode="graph", min_seconds=MIN_TIMED_SECONDS, shards=1):
+    """Average duration of one of `n` back-to-back launches (launch(i, hip_stream), or with
+    shards > 1 launch(i, hip_stream, k) for every shard k, shard k's chain on its own stream
+    forked from the launch stream and joined back after the n launches), captured in a graph as
+    the timed region is, replayed until at least `min_seconds` are timed; HIP events on the
+    launch stream.  Returns (ms per launch of the whole batch, launches timed)."""
     import torch
 
+    subs = [torch.cuda.Stream(dev) for _ in range(shards - 1)]
+
     def launches(st):
-        sc = ctypes.c_void_p(st.cuda_stream)
+        if shards == 1:
+            sc = ctypes.c_void_p(st.cuda_stream)
+            for i in range(n):
+                launch(i, sc)
+            return
+        for sub in subs:
+            sub.wait_stream(st)
+        scs = [ctypes.c_void_p(x.cuda_stream) for x in [st] + subs]
         for i in range(n):
-            launch(i, sc)
+            for k in range(shards):
+                launch(i, scs[k], k)
+        for sub in subs:
+            st.wait_stream(sub)
     g = None
     if mode == "graph":
         g = torch.cuda.CUDAGraph()
@@ -265,6 +279,21 @@ def extra_configs(args, dev, B):
                 "launches_timed": n, "steps_per_launch": spl,
                 "roofline": roofline_entry(alg, us, B, key, kernel, spl)}
 
+    # the rollout entries as the main line runs them: the batch as S shards of Bs envs, each
+    # shard's launches on its own stream (--stream-shards)
+    S = args.stream_shards if args.stream_shards >= 1 and B % (64 * args.stream_shards) == 0 else 1
+    Bs = B // S
+
+    def shards_of(env, opts, stride, slots, acts):
+        envs = [env] if S == 1 else [
+            BatchedWolvesAndBushesEnv(opts, num_envs=Bs, seed=0x5EED, device=dev, env_id_base=k * Bs, autoreset=True,
+                                      validate_actions=False, plane_stride=stride, wolf_slots=slots)
+            for k in range(S)]
+        if S > 1:
+            for e in envs:
+                e.reset()
+        return envs, acts.view(-1, S, Bs).permute(1, 0, 2).contiguous()
+
     for cfg in ("wide31", "c5", "default"):
         opts, stride, slots, _ = CONFIGS[cfg]
         env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev, autoreset=True,
@@ -276,24 +305,33 @@ def extra_configs(args, dev, B):
         env.reset()
         if cfg == "c5":
             F = int(L.wab_feature_dim(h))
-            feats = torch.empty((T, B, F), dtype=torch.float32, device=dev)
-            rd = torch.empty((T, B), dtype=torch.float32, device=dev)
-            dn = torch.empty((T, B), dtype=torch.uint8, device=dev)
-            ret = torch.empty((T, B), dtype=torch.float32, device=dev)
-            sc = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
-            rseq = _lib.WabObs(None, sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
+            envs, sacts = shards_of(env, opts, stride, slots, acts)
+            bufs = []
+            for k in range(S):
+                sc = torch.empty((3, T, Bs), dtype=torch.uint8, device=dev)
+                bufs.append((_lib.WabObs(None, sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr()),
+                             torch.empty((T, Bs), dtype=torch.float32, device=dev),
+                             torch.empty((T, Bs), dtype=torch.uint8, device=dev),
+                             torch.empty((T, Bs, F), dtype=torch.float32, device=dev),
+                             torch.empty((T, Bs), dtype=torch.float32, device=dev), sc))
 
-            def roll(t, s):
-                _lib.check(L.wab_rollout_features(h, a0 + t * B, T, ctypes.addressof(rseq), rd.data_ptr(),
-                                                  dn.data_ptr(), feats.data_ptr(), 0.99, None, ret.data_ptr(), s),
-                           "wab_rollout_features")
+            def roll(t, s, k=0):
+                rseq, rd, dn, feats, ret, _ = bufs[k]
+                _lib.check(L.wab_rollout_features(envs[k]._h, sacts[k].data_ptr() + t * Bs, T, ctypes.addressof(rseq),
+                                                  rd.data_ptr(), dn.data_ptr(), feats.data_ptr(), 0.99, None,
+                                                  ret.data_ptr(), s), "wab_rollout_features")
             for t in range(0, W, T):
-                roll(t, ctypes.c_void_p(stream.cuda_stream))
-            ms, n = time_launches(lambda i, s: roll(W + i * T, s), NL, dev, stream, args.mode)
-            out["c5_rollout"] = entry(ms * 1e3 / T, c5_rollout_alg_bytes(F, T), "c5_rollout%d" % T,
+                for k in range(S):
+                    roll(t, ctypes.c_void_p(stream.cuda_stream), k)
+            ms, n = time_launches(lambda i, s, k=0: roll(W + i * T, s, k), NL, dev, stream, args.mode, shards=S)
+            out["c5_rollout"] = entry(ms * 1e3 / T, c5_rollout_alg_bytes(F, T),
+                                      "c5_rollout%d" % T + ("_s%d" % S if S > 1 else ""),
                                       "wab_step_small + features + returns, rollout build (wab_rollout_features)",
-                                      T, n, "wab_rollout_features, %d steps per launch (C5: actor_critic.py:185-200)" % T)
-            del feats
+                                      T, n, "wab_rollout_features, %d steps per launch (C5: actor_critic.py:185-200)%s"
+                                      % (T, ", the batch as %d shards of %d envs on %d streams" % (S, Bs, S)
+                                         if S > 1 else ""))
+            out["c5_rollout"]["stream_shards"] = S
+            del bufs, envs
         else:
             pl = torch.empty((T, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
             sc = torch.empty((3, T, B), dtype=torch.uint8, device=dev)
@@ -308,10 +346,34 @@ def extra_configs(args, dev, B):
                 roll(t, ctypes.c_void_p(stream.cuda_stream))
             kname = "wab_step_%s" % L.wab_step_kernel(h).decode()
             if cfg == "wide31":
-                ms, n = time_launches(lambda i, s: roll(W + i * T, s), NL, dev, stream, args.mode)
+                del pl
+                envs, sacts = shards_of(env, opts, stride, slots, acts)
+                bufs = []
+                for k in range(S):
+                    pk = torch.empty((T, Bs, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+                    sk = torch.empty((3, T, Bs), dtype=torch.uint8, device=dev)
+                    bufs.append((_lib.WabObs(pk.data_ptr(), sk[0].data_ptr(), sk[1].data_ptr(), sk[2].data_ptr()),
+                                 torch.empty((T, Bs), dtype=torch.float32, device=dev),
+                                 torch.empty((T, Bs), dtype=torch.uint8, device=dev), pk, sk))
+
+                def sroll(t, s, k=0):
+                    o, rdk, dnk, _, _ = bufs[k]
+                    _lib.check(L.wab_rollout(envs[k]._h, sacts[k].data_ptr() + t * Bs, T, ctypes.addressof(o),
+                                             rdk.data_ptr(), dnk.data_ptr(), s), "wab_rollout")
+                if S > 1:
+                    for t in range(0, W, T):
+                        for k in range(S):
+                            sroll(t, ctypes.c_void_p(stream.cuda_stream), k)
+                ms, n = time_launches(lambda i, s, k=0: sroll(W + i * T, s, k), NL, dev, stream, args.mode, shards=S)
                 out["wide31_rollout"] = entry(ms * 1e3 / T, alg_bytes_per_env_step_rollout(env.W, env.H, T),
-                                              "wide31_rollout%d" % T, kname + ", rollout build", T, n,
-                                              "wab_rollout, %d steps per launch (C3: 31x31 in 32x32 planes)" % T)
+                                              "wide31_rollout%d" % T + ("_s%d" % S if S > 1 else ""),
+                                              kname + ", rollout build", T, n,
+                                              "wab_rollout, %d steps per launch (C3: 31x31 in 32x32 planes)%s"
+                                              % (T, ", the batch as %d shards of %d envs on %d streams" % (S, Bs, S)
+                                                 if S > 1 else ""))
+                out["wide31_rollout"]["stream_shards"] = S
+                del bufs, envs
+                pl = None
             # the per-step surface: one wab_step launch per step, step t's obs into slot t % 32
             # of a ring of [B] buffers (so they reach HBM as a closed loop's would)
             del pl
@@ -751,7 +813,7 @@ def main():
     rollout = args.rollout > 0 and not c5
     T_roll = args.rollout
     B, K, W = args.batch, args.steps, args.warmup
-    S = args.stream_shards if rollout else 1
+    S = args.stream_shards if (rollout or (c5_roll and args.policy != "mlp")) else 1
     if S < 1 or B % (64 * S):
         S = 1  # (whole 64-env groups per shard)
     env = BatchedWolvesAndBushesEnv(opts, num_envs=B, seed=0x5EED, device=dev,
@@ -787,6 +849,32 @@ def main():
     obs_addr = ctypes.addressof(env._obs["struct"])
     a0 = actions.data_ptr()
     rew, done = env.reward.data_ptr(), env.done.data_ptr()
+    # a sharded rollout line: the B envs as S handles of Bs envs (ids contiguous, so the union is
+    # the one-handle batch bit for bit), shard k's launches in order on its own stream
+    Bs = B // S
+    shard_envs = [env] if S == 1 else [
+        BatchedWolvesAndBushesEnv(opts, num_envs=Bs, seed=0x5EED, device=dev,
+                                  env_id_base=env_id_base(rank, B) + k * Bs, autoreset=True,
+                                  validate_actions=False, plane_stride=stride, wolf_slots=slots)
+        for k in range(S)]
+    if S > 1:
+        for e in shard_envs:
+            e.reset()
+    # each shard's actions [W + K][Bs] contiguous (the same random draws, shard-major)
+    shard_actions = actions.view(W + K, S, Bs).permute(1, 0, 2).contiguous() if S > 1 else None
+    shard_streams = [torch.cuda.Stream(dev) for _ in range(S - 1)]
+
+    def shard_chains(t0, n, T, stream, launch):
+        """launch(k, t, hip_stream) for every T-step launch t in [t0, t0 + n) of every shard k,
+        shard 0 on `stream`, the others on their own streams forked from it and joined back"""
+        subs = [stream] + shard_streams
+        for st in shard_streams:
+            st.wait_stream(stream)
+        for t in range(t0, t0 + n, T):
+            for k, st in enumerate(subs):
+                launch(k, t, ctypes.c_void_p(st.cuda_stream))
+        for st in shard_streams:
+            stream.wait_stream(st)
     if c5:
         T = T_roll if c5_roll else C5_SEGMENT
         F = int(L.wab_feature_dim(h))
@@ -815,6 +903,15 @@ def main():
         policy = None
         if args.policy == "mlp":
             policy = make_policy(F, env.n_actions, dev)
+        c5_shard = []  # per shard: scalars WabObs, reward, done, features, returns (+ keepalive)
+        if c5_roll and S > 1:
+            for k in range(S):
+                sc_k = torch.empty((3, T, Bs), dtype=torch.uint8, device=dev)
+                c5_shard.append((_lib.WabObs(None, sc_k[0].data_ptr(), sc_k[1].data_ptr(), sc_k[2].data_ptr()),
+                                 torch.empty((T, Bs), dtype=torch.float32, device=dev),
+                                 torch.empty((T, Bs), dtype=torch.uint8, device=dev),
+                                 torch.empty((T, Bs, F), dtype=torch.float32, device=dev),
+                                 torch.empty((T, Bs), dtype=torch.float32, device=dev), sc_k))
 
         def run(t0, n, stream):
             s = ctypes.c_void_p(stream.cuda_stream)
@@ -827,6 +924,12 @@ def main():
                     if i == T - 1:
                         _lib.check(L.wab_discounted_returns_exact(h, r0, d0, T, B, 0.99, None, ret0, s),
                                    "wab_discounted_returns_exact")
+                return
+            if c5_roll and S > 1:  # the shards' segments on their streams
+                shard_chains(t0, n, T, stream, lambda k, t, sk: _lib.check(L.wab_rollout_features(
+                    shard_envs[k]._h, shard_actions[k].data_ptr() + t * Bs, T, ctypes.addressof(c5_shard[k][0]),
+                    c5_shard[k][1].data_ptr(), c5_shard[k][2].data_ptr(), c5_shard[k][3].data_ptr(), 0.99, None,
+                    c5_shard[k][4].data_ptr(), sk), "wab_rollout_features"))
                 return
             if c5_roll:  # one launch per segment: T fused steps and the segment's returns
                 for t in range(t0, t0 + n, T):
@@ -841,18 +944,8 @@ def main():
                                "wab_discounted_returns_exact")
     elif rollout:
         T = args.rollout
-        # the timed workload: the B envs as S shards of Bs envs (ids contiguous, so the union is the
-        # one-handle batch bit for bit), shard k's T-step launches in order on its own stream
-        Bs = B // S
-        shard_envs = [env] if S == 1 else [
-            BatchedWolvesAndBushesEnv(opts, num_envs=Bs, seed=0x5EED, device=dev,
-                                      env_id_base=env_id_base(rank, B) + k * Bs, autoreset=True,
-                                      validate_actions=False, plane_stride=stride, wolf_slots=slots)
-            for k in range(S)]
-        for e in shard_envs[1 if S == 1 else 0:]:
-            e.reset()
-        # each shard's actions [W + K][Bs] contiguous (the same random draws, shard-major)
-        shard_actions = actions.view(W + K, S, Bs).permute(1, 0, 2).contiguous()
+        if S == 1:
+            shard_actions = actions.view(1, W + K, B)
         shard_bufs = []
         for k, e in enumerate(shard_envs):
             pl = torch.empty((T, Bs, 3, env.W, env.S), dtype=torch.uint8, device=dev)
@@ -861,18 +954,13 @@ def main():
             dn = torch.empty((T, Bs), dtype=torch.uint8, device=dev)
             o = _lib.WabObs(pl.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
             shard_bufs.append((e._h, shard_actions[k].data_ptr(), o, pl, sc, rw, dn))
-        shard_streams = [torch.cuda.Stream(dev) for _ in range(S - 1)]
 
         def run(t0, n, stream):
-            subs = [stream] + shard_streams  # (forked from `stream`, joined back at the end)
-            for st in shard_streams:
-                st.wait_stream(stream)
-            for t in range(t0, t0 + n, T):
-                for (hk, ak, o, pl, sc, rw, dn), st in zip(shard_bufs, subs):
-                    _lib.check(L.wab_rollout(hk, ak + t * Bs, T, ctypes.addressof(o), rw.data_ptr(), dn.data_ptr(),
-                                             ctypes.c_void_p(st.cuda_stream)), "wab_rollout")
-            for st in shard_streams:
-                stream.wait_stream(st)
+            def launch(k, t, sk):
+                hk, ak, o, pl, sc, rw, dn = shard_bufs[k]
+                _lib.check(L.wab_rollout(hk, ak + t * Bs, T, ctypes.addressof(o), rw.data_ptr(), dn.data_ptr(), sk),
+                           "wab_rollout")
+            shard_chains(t0, n, T, stream, launch)
     elif args.obs_ring > 0:
         N = args.obs_ring
         ring_planes = torch.empty((N, B, 3, env.W, env.S), dtype=torch.uint8, device=dev)
@@ -916,7 +1004,7 @@ def main():
         print("bench.py: %d steps captured" % K, file=sys.stderr, flush=True)
         # the capture itself did not execute the steps; rewind state by a fresh reset
         env.reset()
-        if rollout and S > 1:
+        if S > 1:
             for e in shard_envs:
                 e.reset()
         run(0, W, stream)
@@ -938,7 +1026,7 @@ def main():
     if world > 1:  # every rank times the same number of steps
         reps = int(max_over_ranks(reps))
 
-    timed_envs = shard_envs if rollout else [env]
+    timed_envs = shard_envs if (rollout or c5_roll) else [env]
 
     def workload_counters():
         out = {}
@@ -1098,6 +1186,7 @@ def main():
                 # the line's kernel is the rollout launch itself (kern_ms: per step from the
                 # timed region); the per-step fused launch is a diagnostic beside it
                 c5_line["rollout_launch_us"] = round(kern_ms * T * 1e3, 3)
+                c5_line["stream_shards"] = S
                 c5_line["per_step_launch_frac"] = round(sf_alg * B / (sf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                 alg = c5_rollout_alg_bytes(F, T)
                 kernel_name = ("wab_step_%s + PragmaticObsWrapper features + returns, rollout build (%d steps "
@@ -1136,7 +1225,7 @@ def main():
                 kernel_name, alg, kern_ms = fk + " (PragmaticObsWrapper + flatten)", feat_alg, feat_ms
             else:
                 kern_ms = step_ms
-    counters = workload_counters() if rollout else env.counters()
+    counters = workload_counters() if (rollout or c5_roll) else env.counters()
     achieved_rank = alg * B / (kern_ms * 1e-3) / 1e9
     per_rank = all_gather_objects({
         "rank": rank, "device": str(dev), "pci": pci_id(dev), "env_steps_per_s": round(B * K / elapsed_rank, 1),
@@ -1175,7 +1264,10 @@ def main():
                                                % (S, B // S) if S > 1 else "")
                                            if rollout else
                                            "; %d-step wab_rollout_features launches (features, reward, done, "
-                                           "returns into [%d, B] rollout buffers)" % (T_roll, T_roll)
+                                           "returns into [%d, B] rollout buffers)%s" % (
+                                               T_roll, T_roll,
+                                               ", the batch as %d shards of %d envs, each on its own HIP stream"
+                                               % (S, B // S) if S > 1 else "")
                                            if c5_roll else
                                            "; one step launch per step, obs into a %d-slot ring" % args.obs_ring
                                            if args.obs_ring > 0 else "; one step launch per step"),

@@ -136,45 +136,68 @@ def test_rollout_features_bench_config_vs_oracle():
     assert c["resets"] > 4 * B
 
 
-def test_headline_stream_shards_equal_one_handle():
-    """The headline line as bench.py runs it (--stream-shards 2): the batch as two handles of
-    B / 2 envs (ids 0.. and B/2..), each shard's 64-step launches on its own HIP stream, running
-    concurrently.  Every step's obs, scalars, reward and done, and the final hidden state, equal
-    one handle of B envs stepped with the same actions (which the test above pins to the oracle)."""
+def _shards_equal_one_handle(opts, stride, slots, launch, keys, seed0):
+    """bench.py's --stream-shards 2: the batch as two handles of B / 2 envs (ids 0.. and B/2..),
+    each shard's launches on its own HIP stream, running concurrently.  Every output of every
+    launch (launch(env, actions) -> dict of [T, ..., B-slice ...] tensors, the env axis at
+    keys[name]), and the final hidden state, equal one handle of B envs stepped with the same
+    actions (which the tests above pin to the oracle)."""
     import torch
 
     from wab_gym_amd.env import BatchedWolvesAndBushesEnv
 
     S, Bs = 2, B // 2
-    mk = lambda n, base: BatchedWolvesAndBushesEnv(None, num_envs=n, seed=SEED, device="cuda:0",  # noqa: E731
+    mk = lambda n, base: BatchedWolvesAndBushesEnv(opts, num_envs=n, seed=SEED, device="cuda:0",  # noqa: E731
                                                    env_id_base=base, autoreset=True, validate_actions=False,
-                                                   wolf_slots=8)
+                                                   plane_stride=stride, wolf_slots=slots)
     one = mk(B, 0)
     shards = [mk(Bs, k * Bs) for k in range(S)]
     for e in [one] + shards:
         e.reset()
     streams = [torch.cuda.Stream() for _ in range(S)]
     for k in range(3):  # three launches: past the turn-80 cap of the first episodes
-        a = _actions(900 + k, one.n_actions)
+        a = _actions(seed0 + k, one.n_actions)
         a_sh = [a[:, j * Bs:(j + 1) * Bs].contiguous() for j in range(S)]
         cur = torch.cuda.current_stream()
         outs = []
         for j, (e, st) in enumerate(zip(shards, streams)):
             st.wait_stream(cur)
             with torch.cuda.stream(st):
-                outs.append(e.rollout(a_sh[j]))
-        planes, scal, rew, done = one.rollout(a)
+                outs.append(launch(e, a_sh[j]))
+        want = launch(one, a)
         for st in streams:
             cur.wait_stream(st)
         torch.cuda.synchronize()
-        for j, (p_, s_, r_, d_) in enumerate(outs):
-            sl = slice(j * Bs, (j + 1) * Bs)
-            assert torch.equal(p_, planes[:, sl]), (k, j, "planes")
-            assert torch.equal(s_, scal[:, :, sl]), (k, j, "scalars")
-            assert torch.equal(r_, rew[:, sl]) and torch.equal(d_, done[:, sl]), (k, j, "reward/done")
-        del outs, planes
+        for j, got in enumerate(outs):
+            for name, axis in keys.items():
+                w = want[name].narrow(axis, j * Bs, Bs)
+                assert torch.equal(got[name], w), (k, j, name)
+        del outs, want
     so = one.state()
     for j, e in enumerate(shards):
         ss = e.state()
         for key in ss:
             assert np.array_equal(ss[key], so[key][j * Bs:(j + 1) * Bs]), (j, key)
+
+
+def _rollout_dict(e, a):
+    planes, scal, rew, done = e.rollout(a)
+    return {"planes": planes, "scalars": scal, "reward": rew, "done": done}
+
+
+def test_headline_stream_shards_equal_one_handle():
+    """The headline line as bench.py runs it: two shards of wab_rollout (small kernel)."""
+    _shards_equal_one_handle(None, 0, 8, _rollout_dict, {"planes": 1, "scalars": 2, "reward": 1, "done": 1}, 900)
+
+
+def test_wide_stream_shards_equal_one_handle():
+    """C3's line as bench.py runs it: two shards of wab_rollout on the wide kernel."""
+    _shards_equal_one_handle({"width": 31, "height": 31}, 32, 32, _rollout_dict,
+                             {"planes": 1, "scalars": 2, "reward": 1, "done": 1}, 910)
+
+
+def test_features_stream_shards_equal_one_handle():
+    """C5's line as bench.py runs it: two shards of wab_rollout_features (features, scalars,
+    reward, done and the segment's returns)."""
+    _shards_equal_one_handle(None, 0, 8, lambda e, a: e.rollout_features(a, gamma=0.99),
+                             {"features": 1, "scalars": 2, "reward": 1, "done": 1, "returns": 1}, 920)

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--shards", type=int, default=2)
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--launches", type=int, default=48)
+    ap.add_argument("--config", default="default", help="bench.py config: default, wide31 or c5")
     args = ap.parse_args()
     import torch
 
@@ -26,22 +27,38 @@ def main():
     dev = torch.device("cuda:0")
     B, T, S, K = args.batch, args.T, args.shards, args.launches
 
+    import bench
+
+    opts, stride, slots, _ = bench.CONFIGS[args.config]
+    c5 = args.config == "c5"
+
     def setup(n, base):
-        env = BatchedWolvesAndBushesEnv(None, num_envs=n, seed=0x5EED, device=dev, env_id_base=base,
-                                        validate_actions=False, wolf_slots=8)
+        env = BatchedWolvesAndBushesEnv(opts, num_envs=n, seed=0x5EED, device=dev, env_id_base=base,
+                                        validate_actions=False, wolf_slots=slots, plane_stride=stride)
         env.reset()
         acts = torch.randint(0, env.n_actions, (T, n), device=dev).to(torch.int8)
-        pl = torch.empty((T, n, 3, env.W, env.S), dtype=torch.uint8, device=dev)
+        pl = None if c5 else torch.empty((T, n, 3, env.W, env.S), dtype=torch.uint8, device=dev)
         sc = torch.empty((3, T, n), dtype=torch.uint8, device=dev)
         rw = torch.empty((T, n), dtype=torch.float32, device=dev)
         dn = torch.empty((T, n), dtype=torch.uint8, device=dev)
-        o = _lib.WabObs(pl.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
-        return env, acts, pl, sc, rw, dn, o
+        o = _lib.WabObs(None if c5 else pl.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr())
+        extra = None
+        if c5:
+            F = int(L.wab_feature_dim(env._h))
+            extra = (torch.empty((T, n, F), dtype=torch.float32, device=dev),
+                     torch.empty((T, n), dtype=torch.float32, device=dev))
+        return env, acts, (pl, extra), sc, rw, dn, o
 
     def launch_all(shards, streams, k):
         for (env, acts, pl, sc, rw, dn, o), st in zip(shards, streams):
-            _lib.check(L.wab_rollout(env._h, acts.data_ptr(), T, ctypes.addressof(o), rw.data_ptr(),
-                                     dn.data_ptr(), ctypes.c_void_p(st.cuda_stream)), "wab_rollout")
+            if c5:
+                f, ret = pl[1]
+                _lib.check(L.wab_rollout_features(env._h, acts.data_ptr(), T, ctypes.addressof(o), rw.data_ptr(),
+                                                  dn.data_ptr(), f.data_ptr(), 0.99, None, ret.data_ptr(),
+                                                  ctypes.c_void_p(st.cuda_stream)), "wab_rollout_features")
+            else:
+                _lib.check(L.wab_rollout(env._h, acts.data_ptr(), T, ctypes.addressof(o), rw.data_ptr(),
+                                         dn.data_ptr(), ctypes.c_void_p(st.cuda_stream)), "wab_rollout")
 
     def run(shards, streams):
         for it in range(2):  # warm-up, then timed
@@ -89,8 +106,8 @@ def main():
     sts = [torch.cuda.Stream(dev) for _ in range(S)]
     usS = run(sh, sts)
     gS = run_graph(sh)
-    print("B=%d T=%d: one handle %.3f us per step (graph %.3f); %d shards on %d streams %.3f (graph %.3f)"
-          % (B, T, us1, g1, S, S, usS, gS))
+    print("%s B=%d T=%d: one handle %.3f us per step (graph %.3f); %d shards on %d streams %.3f (graph %.3f)"
+          % (args.config, B, T, us1, g1, S, S, usS, gS))
 
 
 if __name__ == "__main__":
