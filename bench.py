@@ -25,6 +25,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -157,6 +158,18 @@ def torus_actions(T, B, NO, NW, NB, dev, gen):
         r = torch.randint(0, 1 << 30, (t1 - t0, B, N), device=dev, generator=gen, dtype=torch.int32)
         out[t0:t1] = (r % hi).to(torch.int8)
     return out
+
+
+def finite(x):
+    """The line with every non-finite float (a surface the run did not measure) as null, so
+    it is strict JSON."""
+    if isinstance(x, float) and not math.isfinite(x):
+        return None
+    if isinstance(x, dict):
+        return {k: finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [finite(v) for v in x]
+    return x
 
 
 def time_launches(launch, n, dev, stream, mode="graph", min_seconds=MIN_TIMED_SECONDS, shards=1):
@@ -564,7 +577,7 @@ def run_torus(args, dev, rank, world):
             cores = host_cores()
             line["cpu_baseline"] = torus_cpu_baseline(args.cpu_seconds, cores["used"])
             line["cpu_baseline"]["host"] = cores
-        print(json.dumps(line), flush=True)
+        print(json.dumps(finite(line), allow_nan=False), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -1316,7 +1329,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, cores["used"], c5)
             line["cpu_baseline"]["host"] = cores
             line["cpu_baseline_1t"] = cpu_baseline(opts, stride, args.cpu_seconds / 2, 1, c5)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(finite(line), allow_nan=False), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
