@@ -94,8 +94,8 @@ struct TParams {
   // own act (wab2_get_obs: o = [i, i + 1), nothing acts; wab2_take_action: a = [i, i + 1))
   int32_t a0, a1, o0, o1;
   // (set by launch_torus) ceil(2^20 / n) for the window's n mover and n bush observers, so
-  // that q / n = (q * magic) >> 20 for q < 2048; ceil(2^16 / (R / 16))
-  uint32_t magic_m, magic_b, magic_cr;
+  // that q / n = (q * magic) >> 20 for q < 2048; ceil(2^16 / (R / 16)); ceil(2^20 / N)
+  uint32_t magic_m, magic_b, magic_cr, magic_n;
 };
 
 __device__ __forceinline__ int pymod(int a, int m) {
@@ -564,11 +564,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const uint8_t* row = s.bf1 + w * NBp;  // (bushes observe after every ostrich's eat)
           const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
           const uint64_t fb = (uint64_t)__double_as_longlong((double)row[i - NM]);
-          if (whole_turn && on) {  // a bush: reward 0, done (World.py:84-85, :339-343)
-            const int64_t o = (int64_t)t * p.B * N + (wg0 + w) * N + i;
-            p.reward[o] = 0.0f;
-            p.done[o] = 1;
-          }
           const uint64_t v64 = (uint64_t)vis << 8;  // (bit NM + b + 8: bush b, b >= -8)
           for (int half = 0; half < 2; ++half) {
             const int q0 = rnd * 64 + 32 * half;
@@ -707,14 +702,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             food = s.food[i * kWorlds + w];
           }
           const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
-          if (whole_turn && on && hf == 0) {
-            float rew;
-            uint8_t dn;
-            reward_done(type, status, type == T_WOLF && s.gain[i * kWorlds + w] ? food + p.wff : food, rew, dn);
-            const int64_t o = (int64_t)t * p.B * N + (wg0 + w) * N + i;
-            p.reward[o] = rew;
-            p.done[o] = dn;
-          }
           uint8_t* rec = stage + (lane & 31) * R;
           if (hf == 0) {
             const uint64_t fb = (uint64_t)__double_as_longlong(food);
@@ -780,6 +767,26 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
           }
           __builtin_amdgcn_wave_barrier();
+        }
+      }
+      // reward and done of a whole turn's (world, entity) items (compute_reward World.py:21-22,
+      // 54-58, 84-85; is_entity_done :339-343), from the tables as the observers saw them (phase
+      // C updates them after the barrier): the workgroup's [64][N] slice of [B][N] is contiguous,
+      // so consecutive lanes store consecutive floats and bytes
+      if (whole_turn) {
+        const int64_t o = (int64_t)t * p.B * N + wg0 * N;
+        for (int q = tid; q < nvalid * N; q += kThreads) {
+          const int w = (int)(((uint32_t)q * p.magic_n) >> 20), e = q - w * N;
+          const int type = e < NO ? T_OSTRICH : e < NM ? T_WOLF : T_BUSH;
+          float rew = 0.0f;
+          uint8_t dn = 1;
+          if (type != T_BUSH) {
+            const double food = s.food[e * kWorlds + w];
+            const int status = type == T_OSTRICH ? ost_status(s.ost[e * kWorlds + w]) : 0;
+            reward_done(type, status, type == T_WOLF && s.gain[e * kWorlds + w] ? food + p.wff : food, rew, dn);
+          }
+          p.reward[o + q] = rew;
+          p.done[o + q] = dn;
         }
       }
     }
@@ -1023,6 +1030,7 @@ void launch_torus(const wab2_handle* h, const TParams& p0, hipStream_t stream) {
   p.magic_m = magic20(std::min(p.o1, p.NM) - p.o0);
   p.magic_b = magic20(p.o1 - std::max(p.o0, p.NM));
   p.magic_cr = (uint32_t)((65536 + p.R / 16 - 1) / (p.R / 16));
+  p.magic_n = magic20(p.N);
   switch ((p.N + 3) / 4) {
     case 1: hipLaunchKernelGGL(wab2::wab_torus_kernel<1>, grid, block, h->lds, stream, p); break;
     case 2: hipLaunchKernelGGL(wab2::wab_torus_kernel<2>, grid, block, h->lds, stream, p); break;
