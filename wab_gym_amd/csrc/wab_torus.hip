@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,6 +42,26 @@
 // bit 8 phase C, bit 16 the bush observers' rounds, bit 32 the movers' rounds, bit 64 phase A.
 #ifndef WAB2_ABLATE
 #define WAB2_ABLATE 0
+#endif
+// Diagnostic build only (tools/torus_stamps.py): WAB2_STAMPS=1 records s_memtime at the phase
+// boundaries of the middle turn, per wave, into the buffer whose address the host reads from
+// the WAB2_STAMPS_PTR environment variable ([n_blocks][4 waves][16] u64; the product library
+// reads no environment variable).
+#ifndef WAB2_STAMPS
+#define WAB2_STAMPS 0
+#endif
+#if WAB2_STAMPS
+#define WAB2_STAMP(k)                                                                                 \
+  do {                                                                                                \
+    if (t == p0.T / 2) {                                                                              \
+      const uint64_t ts_ = __builtin_amdgcn_s_memtime();                                              \
+      if (lane == 0) p0.stamps[((int64_t)blockIdx.x * 4 + wave) * 16 + (k)] = ts_;                    \
+    }                                                                                                 \
+  } while (0)
+#else
+#define WAB2_STAMP(k) \
+  do {                \
+  } while (0)
 #endif
 
 namespace wab2 {
@@ -96,6 +117,9 @@ struct TParams {
   // (set by launch_torus) ceil(2^20 / n) for the window's n mover and n bush observers, so
   // that q / n = (q * magic) >> 20 for q < 2048; ceil(2^16 / (R / 16)); ceil(2^20 / N)
   uint32_t magic_m, magic_b, magic_cr, magic_n;
+#if WAB2_STAMPS
+  unsigned long long* stamps;
+#endif
 };
 
 __device__ __forceinline__ int pymod(int a, int m) {
@@ -378,6 +402,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
 
   int64_t resets = 0;
   for (int t = 0; t < T; ++t) {
+    WAB2_STAMP(0);
     // ================= phase A: the sequential part of the turn, one lane per world
     if (WAB2_ABLATE & 64) {
     } else if (wave == 0) {
@@ -440,30 +465,43 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         }
       }
       const uint32_t vis0 = vis;  // (before this launch's kills)
-      for (int m = max(a0, NO); m < min(a1, NM); ++m) {
-        const uint32_t np = moved(s.omod[m * kWorlds + w], (int)(int8_t)A[w * na + m - a0], W, H);
-        reinterpret_cast<uint16_t*>(posw + m)[1] = (uint16_t)np;
-        uint32_t cand = 0;
+      // eight wolves at a time: their moves' LDS reads issued together, then the kills in id order
+      const int m0 = max(a0, NO), m1 = min(a1, NM);
+      for (int mb = m0; mb < m1; mb += 8) {
+        uint32_t np8[8];
 #pragma unroll
-        for (int k = 0; k < kOMax; ++k) cand |= (uint32_t)((vis >> k & 1u) && opos[k] == np) << k;
-        uint32_t gain = 0;
-        if (cand) {
-          const int n = __builtin_popcount(cand);
-          const int j = keyed_below(ek, SITE_T_KILL, turn, m, 0, (uint32_t)n);
-          uint32_t c = cand;
-          for (int r = 0; r < j; ++r) c &= c - 1;
-          kills |= c & (0u - c);  // the j-th visible ostrich of the tile: status 2 (:114)
-          gain = 1;
-          // `loc[j, "Visible"] = False` (:115): the frame LABEL j, an ostrich id since the
-          // ostriches were created first
-#pragma unroll
-          for (int k = 0; k < kOMax; ++k)
-            if (k == j && (vis >> k & 1u)) {
-              vis &= ~(1u << k);
-              hid_by[k] = (uint32_t)m;
-            }
+        for (int jj = 0; jj < 8; ++jj) {
+          const int m = min(mb + jj, m1 - 1);
+          np8[jj] = moved(s.omod[m * kWorlds + w], (int)(int8_t)A[w * na + m - a0], W, H);
         }
-        s.gain[m * kWorlds + w] = (uint8_t)gain;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int m = mb + jj;
+          if (m >= m1) break;
+          const uint32_t np = np8[jj];
+          reinterpret_cast<uint16_t*>(posw + m)[1] = (uint16_t)np;
+          uint32_t cand = 0;
+#pragma unroll
+          for (int k = 0; k < kOMax; ++k) cand |= (uint32_t)((vis >> k & 1u) && opos[k] == np) << k;
+          uint32_t gain = 0;
+          if (cand) {
+            const int n = __builtin_popcount(cand);
+            const int j = keyed_below(ek, SITE_T_KILL, turn, m, 0, (uint32_t)n);
+            uint32_t c = cand;
+            for (int r = 0; r < j; ++r) c &= c - 1;
+            kills |= c & (0u - c);  // the j-th visible ostrich of the tile: status 2 (:114)
+            gain = 1;
+            // `loc[j, "Visible"] = False` (:115): the frame LABEL j, an ostrich id since the
+            // ostriches were created first
+#pragma unroll
+            for (int k = 0; k < kOMax; ++k)
+              if (k == j && (vis >> k & 1u)) {
+                vis &= ~(1u << k);
+                hid_by[k] = (uint32_t)m;
+              }
+          }
+          s.gain[m * kWorlds + w] = (uint8_t)gain;
+        }
       }
 #pragma unroll
       for (int k = 0; k < kOMax; ++k)
@@ -505,7 +543,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       WAB2_PHASE_PARAMS;
       fetch_actions_wave(p, t + 1, wg0, nvalid, (t & 1) ? s.act0 : s.act1, lane);
     }
+    WAB2_STAMP(1);
     lds_barrier();
+    WAB2_STAMP(2);
 
     // ================= phase B: observation records (and, for a whole turn, reward and done).
     // Two classes of observers, each in rounds of 32 (world, observer) items per wave: the
@@ -599,6 +639,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           }
         }
       }
+      WAB2_STAMP(3);
       // ---- the movers
 #pragma unroll
       for (int cls = 1; cls < 2; ++cls) {
@@ -769,28 +810,31 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           __builtin_amdgcn_wave_barrier();
         }
       }
+      WAB2_STAMP(4);
       // reward and done of a whole turn's (world, entity) items (compute_reward World.py:21-22,
       // 54-58, 84-85; is_entity_done :339-343), from the tables as the observers saw them (phase
       // C updates them after the barrier): the workgroup's [64][N] slice of [B][N] is contiguous,
       // so consecutive lanes store consecutive floats and bytes
       if (whole_turn) {
         const int64_t o = (int64_t)t * p.B * N + wg0 * N;
+        // (branch-free: the lanes of one store hold every entity type; reward_done's cases as
+        // selects, the table reads clamped into their tables)
         for (int q = tid; q < nvalid * N; q += kThreads) {
           const int w = (int)(((uint32_t)q * p.magic_n) >> 20), e = q - w * N;
-          const int type = e < NO ? T_OSTRICH : e < NM ? T_WOLF : T_BUSH;
-          float rew = 0.0f;
-          uint8_t dn = 1;
-          if (type != T_BUSH) {
-            const double food = s.food[e * kWorlds + w];
-            const int status = type == T_OSTRICH ? ost_status(s.ost[e * kWorlds + w]) : 0;
-            reward_done(type, status, type == T_WOLF && s.gain[e * kWorlds + w] ? food + p.wff : food, rew, dn);
-          }
-          p.reward[o + q] = rew;
-          p.done[o + q] = dn;
+          const int em = min(e, NM - 1), eo = min(e, NO - 1);
+          const double food = NM > 0 ? s.food[em * kWorlds + w] : 0.0;
+          const bool wolf_fed = (NM > 0 ? s.gain[em * kWorlds + w] : 0u) != 0u;
+          const bool alive = NO > 0 && ost_status(s.ost[eo * kWorlds + w]) == 0;
+          const bool ost = e < NO, wolf = e >= NO && e < NM;
+          const bool wolf_rew = (wolf_fed ? food + p.wff : food) > 10.0;
+          p.reward[o + q] = (ost ? alive : wolf && wolf_rew) ? 1.0f : 0.0f;
+          p.done[o + q] = (uint8_t)(ost ? !alive : !wolf);
         }
       }
     }
+    WAB2_STAMP(5);
     lds_barrier();
+    WAB2_STAMP(6);
 
     // ================= phase C: the launch's end, one lane per (entity, world): the acting
     // entities' moves, roles and food, every ostrich's kills, the bushes' food, the autoreset
@@ -804,12 +848,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const bool acts = e >= a0 && e < a1;
         if (acts) s.pos[w * Np + e] >>= 16;  // the frame X/Y after the act (a reset leaves it)
         const int a = acts ? (int)(int8_t)A[w * na + e - a0] : -1;
-        int nx = 0, ny = 0;
-        if (epr) {  // reset_environment: randint(0, W), randint(0, H) (WAB_Environment2_Single.py:45-46)
-          const uint64_t ek = world_key(p, wg0 + w, epr);
-          nx = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)W + 1u);
-          ny = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)H + 1u);
-        }
         if (e < NM) {
           int2 xy = s.oxy[e * kWorlds + w];
           xy.x += move_dx(a);
@@ -841,17 +879,14 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             p.reward[(int64_t)(wg0 + w) * na + e - a0] = rew;
             p.done[(int64_t)(wg0 + w) * na + e - a0] = dn;
           }
-          if (epr) {
-            xy = make_int2(nx, ny);
-            om = (uint32_t)wrap1(nx, W) | ((uint32_t)wrap1(ny, H) << 8);
+          if (!epr) {  // (a reset world's new positions: the loop below)
+            s.oxy[e * kWorlds + w] = xy;
+            s.omod[e * kWorlds + w] = (uint16_t)om;
           }
-          s.oxy[e * kWorlds + w] = xy;
-          s.omod[e * kWorlds + w] = (uint16_t)om;
           s.food[e * kWorlds + w] = f;
         } else {
           const int b = e - NM;
           s.bf0[w * NBp + b] = epr ? (uint8_t)p.fpb : s.bf1[w * NBp + b];
-          if (epr) s.bxy[b * kWorlds + w] = (uint16_t)(nx | (ny << 8));
           if (!whole_turn && acts && w < nvalid) {
             p.reward[(int64_t)(wg0 + w) * na + e - a0] = 0.0f;
             p.done[(int64_t)(wg0 + w) * na + e - a0] = 1;
@@ -862,8 +897,30 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           if (epr) s.ep[w] = epr;
         }
       }
+      // reset_environment's new positions, randint(0, W), randint(0, H) per entity
+      // (WAB_Environment2_Single.py:45-46), for the worlds that reset (about one in 70 per
+      // turn): a loop over those worlds, lane e drawing entity e's, instead of every lane of a
+      // wave taking the draws' path whenever one of its 64 worlds resets
+      if (!(WAB2_ABLATE & 8)) {
+        for (uint64_t m = __ballot(s.ep_reset[lane] != 0u); m; m &= m - 1) {
+          const int w = __builtin_ctzll(m);
+          const uint64_t ek = world_key(p, wg0 + w, s.ep_reset[w]);
+          for (int e = tid; e < N; e += kThreads) {
+            const int nx = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)W + 1u);
+            const int ny = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)H + 1u);
+            if (e < NM) {
+              s.oxy[e * kWorlds + w] = make_int2(nx, ny);
+              s.omod[e * kWorlds + w] = (uint16_t)((uint32_t)wrap1(nx, W) | ((uint32_t)wrap1(ny, H) << 8));
+            } else {
+              s.bxy[(e - NM) * kWorlds + w] = (uint16_t)(nx | (ny << 8));
+            }
+          }
+        }
+      }
     }
+    WAB2_STAMP(7);
     lds_barrier();
+    WAB2_STAMP(8);
   }
 
   // ---- epilogue: LDS tables -> state
@@ -1031,6 +1088,9 @@ void launch_torus(const wab2_handle* h, const TParams& p0, hipStream_t stream) {
   p.magic_b = magic20(p.o1 - std::max(p.o0, p.NM));
   p.magic_cr = (uint32_t)((65536 + p.R / 16 - 1) / (p.R / 16));
   p.magic_n = magic20(p.N);
+#if WAB2_STAMPS
+  p.stamps = (unsigned long long*)(uintptr_t)strtoull(getenv("WAB2_STAMPS_PTR") ? getenv("WAB2_STAMPS_PTR") : "0", nullptr, 0);
+#endif
   switch ((p.N + 3) / 4) {
     case 1: hipLaunchKernelGGL(wab2::wab_torus_kernel<1>, grid, block, h->lds, stream, p); break;
     case 2: hipLaunchKernelGGL(wab2::wab_torus_kernel<2>, grid, block, h->lds, stream, p); break;
