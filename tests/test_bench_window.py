@@ -44,3 +44,12 @@ def test_policy_mode_argument_checks():
     assert r.returncode != 0 and "--config c5" in r.stderr
     r = _run("--config", "c5", "--policy", "mlp", "--rollout", "64", "--no-cpu")
     assert r.returncode != 0 and "one launch per step" in r.stderr
+
+
+def test_bench_line_is_strict_json():
+    # a surface the run did not measure (NaN) is null in the printed line, never a bare NaN
+    import json
+
+    line = {"a": float("nan"), "b": [1.0, float("inf")], "c": {"d": float("-inf"), "e": 2}, "f": (3.0,)}
+    out = json.loads(json.dumps(bench.finite(line), allow_nan=False))
+    assert out == {"a": None, "b": [1.0, None], "c": {"d": None, "e": 2}, "f": [3.0]}

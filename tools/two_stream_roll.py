@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--launches", type=int, default=48)
     ap.add_argument("--config", default="default", help="bench.py config: default, wide31 or c5")
+    ap.add_argument("--stagger", action="store_true",
+                    help="odd shards start (and end) with a T/2-step launch, so the shards' launch ends alternate")
     args = ap.parse_args()
     import torch
 
@@ -49,16 +51,20 @@ def main():
                      torch.empty((T, n), dtype=torch.float32, device=dev))
         return env, acts, (pl, extra), sc, rw, dn, o
 
+    def launch_one(shard, st, n):
+        env, acts, pl, sc, rw, dn, o = shard
+        if c5:
+            f, ret = pl[1]
+            _lib.check(L.wab_rollout_features(env._h, acts.data_ptr(), n, ctypes.addressof(o), rw.data_ptr(),
+                                              dn.data_ptr(), f.data_ptr(), 0.99, None, ret.data_ptr(),
+                                              ctypes.c_void_p(st.cuda_stream)), "wab_rollout_features")
+        else:
+            _lib.check(L.wab_rollout(env._h, acts.data_ptr(), n, ctypes.addressof(o), rw.data_ptr(),
+                                     dn.data_ptr(), ctypes.c_void_p(st.cuda_stream)), "wab_rollout")
+
     def launch_all(shards, streams, k):
-        for (env, acts, pl, sc, rw, dn, o), st in zip(shards, streams):
-            if c5:
-                f, ret = pl[1]
-                _lib.check(L.wab_rollout_features(env._h, acts.data_ptr(), T, ctypes.addressof(o), rw.data_ptr(),
-                                                  dn.data_ptr(), f.data_ptr(), 0.99, None, ret.data_ptr(),
-                                                  ctypes.c_void_p(st.cuda_stream)), "wab_rollout_features")
-            else:
-                _lib.check(L.wab_rollout(env._h, acts.data_ptr(), T, ctypes.addressof(o), rw.data_ptr(),
-                                         dn.data_ptr(), ctypes.c_void_p(st.cuda_stream)), "wab_rollout")
+        for sh, st in zip(shards, streams):
+            launch_one(sh, st, T)
 
     def run(shards, streams):
         for it in range(2):  # warm-up, then timed
@@ -81,8 +87,17 @@ def main():
                 subs = [cap] + [torch.cuda.Stream(dev) for _ in shards[1:]]
                 for st in subs[1:]:
                     st.wait_stream(cap)
-                for k in range(K):
-                    launch_all(shards, subs, k)
+                if args.stagger and len(shards) > 1:
+                    for k in range(K + 1):
+                        for j, (sh, st) in enumerate(zip(shards, subs)):
+                            if j % 2 == 0:
+                                if k < K:
+                                    launch_one(sh, st, T)
+                            else:
+                                launch_one(sh, st, T // 2 if k in (0, K) else T)
+                else:
+                    for k in range(K):
+                        launch_all(shards, subs, k)
                 for st in subs[1:]:
                     cap.wait_stream(st)
         torch.cuda.synchronize()
@@ -106,8 +121,8 @@ def main():
     sts = [torch.cuda.Stream(dev) for _ in range(S)]
     usS = run(sh, sts)
     gS = run_graph(sh)
-    print("%s B=%d T=%d: one handle %.3f us per step (graph %.3f); %d shards on %d streams %.3f (graph %.3f)"
-          % (args.config, B, T, us1, g1, S, S, usS, gS))
+    print("%s%s B=%d T=%d: one handle %.3f us per step (graph %.3f); %d shards on %d streams %.3f (graph %.3f)"
+          % (args.config, " (staggered)" if args.stagger else "", B, T, us1, g1, S, S, usS, gS))
 
 
 if __name__ == "__main__":
