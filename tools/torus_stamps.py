@@ -9,7 +9,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-NAMES = ["A work", "A barrier", "bush rounds", "mover rounds", "reward/done", "B barrier", "C work", "C barrier"]
+NAMES = ["A work", "A barrier", "bush (W0-1)", "mover+bush(2-3)", "reward/done", "B barrier", "C work", "C barrier"]
 
 
 def main():
