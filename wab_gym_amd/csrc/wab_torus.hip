@@ -355,8 +355,9 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
 }
 
 // NKK = ceil(N / 4): dword-pair groups of the delta array.  CNO, CNW, CNB > 0: an instance for
-// those entity counts, whose table layout, record size and loop bounds are compile-time
-// constants (the benched 1 / 8 / 16 world); 0: the counts from the parameters.
+// whole turns (windows [0, N)) of those entity counts, whose table layout, record size, loop
+// bounds and divisions are compile-time constants (the benched 1 / 8 / 16 world); 0: the counts
+// and windows from the parameters.
 template <int NKK, int CNO = 0, int CNW = 0, int CNB = 0>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) wab_torus_kernel(TParams p0) {
   constexpr bool kFixed = CNO + CNW + CNB > 0;
@@ -374,7 +375,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   const int NB = kFixed ? CNB : p.NB, R = kFixed ? (24 + 2 * kN + CNB + 15) / 16 * 16 : p.R;  \
   const int W = p.W, H = p.H;                                                             \
   const Lds s = lds_tables(smem, N, NO, NM, NB, R);                                       \
-  const int nent = N * kWorlds, a0 = p.a0, a1 = p.a1, na = a1 - a0;                       \
+  const int nent = N * kWorlds, a0 = kFixed ? 0 : p.a0, a1 = kFixed ? N : p.a1, na = a1 - a0; \
+  const int wo0 = kFixed ? 0 : p.o0, wo1 = kFixed ? N : p.o1;                             \
+  const uint32_t magic_m = kFixed ? ((1u << 20) + CNO + CNW - 1) / (CNO + CNW) : p.magic_m; \
+  const uint32_t magic_b = kFixed ? ((1u << 20) + CNB - 1) / CNB : p.magic_b;              \
+  const uint32_t magic_n = kFixed ? ((1u << 20) + kN - 1) / kN : p.magic_n;               \
+  const uint32_t magic_cr = kFixed ? (65536u + R / 16 - 1) / (R / 16) : p.magic_cr;       \
+  (void)wo0; (void)wo1; (void)magic_m; (void)magic_b; (void)magic_n; (void)magic_cr;      \
   const int Np = pos_row(N), NBp = bush_row(NB);                                          \
   (void)NO; (void)NM; (void)NB; (void)R; (void)W; (void)H; (void)nent; (void)na; (void)Np; (void)NBp
 
@@ -564,7 +571,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     // round's 32 records fit the wave's LDS stage and every lane is busy.
     {
       WAB2_PHASE_PARAMS;
-      const int o0 = p.o0, no = p.o1 - p.o0;
+      const int o0 = wo0, no = wo1 - wo0;
       uint8_t* stage = s.stage + wave * 32 * R;
       const int64_t item0 = wg0 * no;  // first record of the workgroup in [B][no]
       uint8_t* obs_t = p.obs + (int64_t)t * p.B * no * R;
@@ -588,14 +595,14 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         // ---- the bush observers: one lane per (world, bush) item, 64 items per round, their
         // records staged and stored in two halves of 32
         {
-          const int c0 = max(o0, NM), nc = max(0, p.o1 - c0);
+          const int c0 = max(o0, NM), nc = max(0, wo1 - c0);
           const int nitems = (WAB2_ABLATE & 16) ? 0 : nvalid * nc;
           const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
           for (int rnd = wave; rnd * 64 < nitems; rnd += 4) {
             const int q = rnd * 64 + lane;
             const bool on = q < nitems;
             const int qc = on ? q : nitems - 1;
-            const int w = (int)(((uint32_t)qc * p.magic_b) >> 20);
+            const int w = (int)(((uint32_t)qc * magic_b) >> 20);
             const int i = c0 + qc - w * nc;
             const uint32_t* posw = s.pos + w * Np;
             const uint32_t tgt = posw[i] & 0xFFFFu;  // (its frame X/Y before its act)
@@ -639,12 +646,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               __builtin_amdgcn_wave_barrier();
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
               const int chunks = min(32, nitems - q0) * CR;
-              const int w0r = (int)(((uint32_t)q0 * p.magic_b) >> 20);
+              const int w0r = (int)(((uint32_t)q0 * magic_b) >> 20);
               uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;
               for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-                const int r = (int)(((uint32_t)c * p.magic_cr) >> 16);
+                const int r = (int)(((uint32_t)c * magic_cr) >> 16);
                 const int qq = q0 + r;
-                const int ww = (int)(((uint32_t)qq * p.magic_b) >> 20);
+                const int ww = (int)(((uint32_t)qq * magic_b) >> 20);
                 const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
                 const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
                 __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
@@ -660,9 +667,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       for (int cls = 1; cls < 2; ++cls) {
         const bool bush = cls == 0;
         // the class's observers [c0, c1) of the window
-        const int c0 = bush ? max(o0, NM) : o0, c1 = bush ? p.o1 : min(p.o1, NM);
+        const int c0 = bush ? max(o0, NM) : o0, c1 = bush ? wo1 : min(wo1, NM);
         const int nc = max(0, c1 - c0);
-        const uint32_t magic = bush ? p.magic_b : p.magic_m;  // q / nc = (q * magic) >> 20
+        const uint32_t magic = bush ? magic_b : magic_m;  // q / nc = (q * magic) >> 20
         const int nitems = (WAB2_ABLATE & (bush ? 16 : 32)) ? 0 : nvalid * nc;
         for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
           const int q = rnd * 32 + (lane & 31);
@@ -815,7 +822,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int w0r = (int)(((uint32_t)q0 * magic) >> 20);  // the round's first world
           uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;  // its first record
           for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-            const int r = (int)(((uint32_t)c * p.magic_cr) >> 16);  // stage slot: c / CR
+            const int r = (int)(((uint32_t)c * magic_cr) >> 16);  // stage slot: c / CR
             const int qq = q0 + r;
             const int ww = (int)(((uint32_t)qq * magic) >> 20);
             const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
@@ -830,14 +837,14 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         // ---- the bush observers: one lane per (world, bush) item, 64 items per round, their
         // records staged and stored in two halves of 32
         {
-          const int c0 = max(o0, NM), nc = max(0, p.o1 - c0);
+          const int c0 = max(o0, NM), nc = max(0, wo1 - c0);
           const int nitems = (WAB2_ABLATE & 16) ? 0 : nvalid * nc;
           const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
           for (int rnd = wave; rnd * 64 < nitems; rnd += 4) {
             const int q = rnd * 64 + lane;
             const bool on = q < nitems;
             const int qc = on ? q : nitems - 1;
-            const int w = (int)(((uint32_t)qc * p.magic_b) >> 20);
+            const int w = (int)(((uint32_t)qc * magic_b) >> 20);
             const int i = c0 + qc - w * nc;
             const uint32_t* posw = s.pos + w * Np;
             const uint32_t tgt = posw[i] & 0xFFFFu;  // (its frame X/Y before its act)
@@ -881,12 +888,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               __builtin_amdgcn_wave_barrier();
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
               const int chunks = min(32, nitems - q0) * CR;
-              const int w0r = (int)(((uint32_t)q0 * p.magic_b) >> 20);
+              const int w0r = (int)(((uint32_t)q0 * magic_b) >> 20);
               uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;
               for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-                const int r = (int)(((uint32_t)c * p.magic_cr) >> 16);
+                const int r = (int)(((uint32_t)c * magic_cr) >> 16);
                 const int qq = q0 + r;
-                const int ww = (int)(((uint32_t)qq * p.magic_b) >> 20);
+                const int ww = (int)(((uint32_t)qq * magic_b) >> 20);
                 const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
                 const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
                 __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
@@ -906,7 +913,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         // (branch-free: the lanes of one store hold every entity type; reward_done's cases as
         // selects, the table reads clamped into their tables)
         for (int q = tid; q < nvalid * N; q += kThreads) {
-          const int w = (int)(((uint32_t)q * p.magic_n) >> 20), e = q - w * N;
+          const int w = (int)(((uint32_t)q * magic_n) >> 20), e = q - w * N;
           const int em = min(e, NM - 1), eo = min(e, NO - 1);
           const double food = NM > 0 ? s.food[em * kWorlds + w] : 0.0;
           const bool wolf_fed = (NM > 0 ? s.gain[em * kWorlds + w] : 0u) != 0u;
@@ -927,7 +934,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     {
       WAB2_PHASE_PARAMS;
       const uint8_t* A = (t & 1) ? s.act1 : s.act0;
-      const bool whole_turn = a0 == 0 && a1 == N && p.o0 == 0 && p.o1 == N;
+      const bool whole_turn = a0 == 0 && a1 == N && wo0 == 0 && wo1 == N;
       for (int q = tid; q < ((WAB2_ABLATE & 8) ? 0 : nent); q += kThreads) {
         const int e = q >> 6, w = q & 63;
         const uint32_t epr = s.ep_reset[w];
@@ -1151,9 +1158,11 @@ std::string validate(const wab2_config* c) {
   return "";
 }
 
-// the benched world's counts (BASELINE config 3: 1 ostrich, 8 wolves, 16 bushes) have an
-// instance of their own with the counts as constants
-bool fixed_counts(const TParams& p) { return p.NO == 1 && p.NW == 8 && p.NB == 16; }
+// whole turns of the benched world's counts (BASELINE config 3: 1 ostrich, 8 wolves, 16 bushes)
+// have an instance of their own with the counts and the (whole) windows as constants
+bool fixed_counts(const TParams& p) {
+  return p.NO == 1 && p.NW == 8 && p.NB == 16 && p.a0 == 0 && p.a1 == p.N && p.o0 == 0 && p.o1 == p.N;
+}
 
 // the kernel instantiation for N entities: ceil(N / 4) dword-pair groups of the delta array
 const void* torus_kernel(const TParams& p) {
