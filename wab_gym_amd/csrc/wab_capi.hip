@@ -25,7 +25,7 @@ template <int SLOTS, int G, bool FEAT, bool ROLL>
 __global__ void wab_step_small(Params p);
 template <int MODE, int SLOTS>
 __global__ void wab_step_wide(Params p);
-template <int SLOTS>
+template <int SLOTS, int FIXW>
 __global__ void wab_rollout_wide(Params p);
 
 __global__ void wab_featurize_kernel(FeatParams p);
@@ -162,6 +162,23 @@ constexpr int kWideRegSlots = 8;
 template <int MODE>
 void* wide_kernel_ptr(int) {
   return reinterpret_cast<void*>(&wab::wab_step_wide<MODE, kWideRegSlots>);
+}
+
+// the wide rollout build: C3's geometry (31 x 31 in 32-byte rows) has an instance with it as
+// constants (wab_rollout_wide<.., 31>), any other the generic one
+bool wide_fixed31(const Params& p) {
+  return p.W == 31 && p.H == 31 && p.S == 32 && p.cw == 15 && p.ch == 15 && p.OB == 3 * 31 * 32 && p.WH == 961 &&
+         p.SL == 31;
+}
+void* wide_roll_kernel(const Params& p) {
+  return wide_fixed31(p) ? reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots, 31>)
+                         : reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots, 0>);
+}
+void launch_rollout_wide(int n_blocks, size_t lds, const Params& p, hipStream_t stream) {
+  if (wide_fixed31(p))
+    hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots, 31>), dim3(n_blocks), dim3(256), lds, stream, p);
+  else
+    hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots, 0>), dim3(n_blocks), dim3(256), lds, stream, p);
 }
 
 template <int G, bool ROLL = false>
@@ -618,8 +635,8 @@ int wab_create(const wab_config* c, int64_t batch, uint64_t seed, int64_t env_id
       if (e == hipSuccess)
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_lds_bytes);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<void*>(&wab::wab_rollout_wide<kWideRegSlots>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wide_roll_lds_bytes);
+      e = hipFuncSetAttribute(wide_roll_kernel(p), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)h->wide_roll_lds_bytes);
   }
   if (e == hipSuccess && h->step_kernel == KERNEL_SMALL)
     for (void* k : {h->small_g11 ? small_kernel_ptr<11>(slots) : small_kernel_ptr<0>(slots),
@@ -665,6 +682,7 @@ int wab_reset(wab_handle* h, const uint8_t* mask, const wab_obs* obs, void* stre
   return rc;
 }
 
+
 int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* reward, uint8_t* done,
              const wab_obs* terminal, void* stream) {
   g_err.clear();
@@ -700,8 +718,7 @@ int wab_step(wab_handle* h, const int8_t* actions, const wab_obs* obs, float* re
     // one buffer 62.5 against 45.9 us.  The results are the same either way.
     if (h->n_blocks == 0) return WAB_OK;
     p.n_steps = 1;
-    hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_roll_lds_bytes,
-                       (hipStream_t)stream, p);
+    launch_rollout_wide(h->n_blocks, h->wide_roll_lds_bytes, p, (hipStream_t)stream);
     HIP_TRY(hipGetLastError());
     return WAB_OK;
   }
@@ -733,8 +750,7 @@ int wab_rollout(wab_handle* h, const int8_t* actions, int32_t T, const wab_obs* 
     ++h->rollout_launches;
     if (h->step_kernel == KERNEL_WIDE) {
       if (h->n_blocks == 0) return WAB_OK;
-      hipLaunchKernelGGL((wab::wab_rollout_wide<kWideRegSlots>), dim3(h->n_blocks), dim3(256), h->wide_roll_lds_bytes,
-                         (hipStream_t)stream, p);
+      launch_rollout_wide(h->n_blocks, h->wide_roll_lds_bytes, p, (hipStream_t)stream);
       HIP_TRY(hipGetLastError());
       return WAB_OK;
     }

@@ -1106,7 +1106,10 @@ __device__ __forceinline__ void wide_step_slice(Params& p, int t) {
 }  // namespace
 
 
-template <int SLOTS>
+// FIXW > 0: an instance for a FIXW x FIXW view in 32-byte rows (C3: 31 x 31), the geometry fields
+// constants after each step's parameter load, so that the layout and index arithmetic fold
+// (the host takes it only for a handle of exactly that geometry); 0: the handle's geometry.
+template <int SLOTS, int FIXW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wab_rollout_wide(Params p0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int64_t g0 = (int64_t)blockIdx.x * 64;
@@ -1155,6 +1158,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     const bool last = t == T - 1;
     const int cur = t & 1;
     Params p = kernel_params(p0);
+    if constexpr (FIXW > 0) {
+      p.W = FIXW;
+      p.H = FIXW;
+      p.S = 32;
+      p.cw = FIXW / 2;
+      p.ch = FIXW / 2;
+      p.OB = 3 * FIXW * 32;
+      p.WH = FIXW * FIXW;
+      p.SL = FIXW;
+    }
     wide_step_slice(p, t);
     const WideRollLayout L = wide_roll_layout(p);
     // (buffers chosen by selects: a runtime index into the layout would put it in scratch)
@@ -1769,7 +1782,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
 #endif
 }
 
-template __global__ void wab_rollout_wide<8>(Params);
+template __global__ void wab_rollout_wide<8, 0>(Params);
+template __global__ void wab_rollout_wide<8, 31>(Params);
 
 #define WAB_WIDE_INST(M, S) template __global__ void wab_step_wide<M, S>(Params);
 WAB_WIDE_INST(MODE_STEP, 8)
