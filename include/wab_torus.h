@@ -17,8 +17,10 @@
  *   wab2_create       <- WAB_Environment2(W, H, options)               WAB_Environment2.py:55-59
  *                        + create_ostriches / create_wolves / create_bushes with random
  *                        positions, in that order                       WAB_Environment2.py:61-110
+ *   wab2_create_at    <- the same with spawn_positions                  WAB_Environment2.py:61-110
  *   wab2_reset        <- reset_environment                              WAB_Environment2.py:113-118
  *                        (WAB_Environment2_Single.reset :36-41, World.reset_world :350-358)
+ *   wab2_reset_at     <- the same with each entity's reset(new_x, new_y) WAB_Environment2_Single.py:36-41
  *   wab2_step         <- one turn: for every entity i in id order,      Env2Tests.py:40-88
  *                        get_obs(i) then take_action(i, a[i])            WAB_Environment2.py:120-134
  *                        (World.get_observations :360-377, perform_entity_action :325-334,
@@ -74,6 +76,8 @@ extern "C" {
 #define WAB2_MAX_ENTITIES 32  /* num_ostriches + num_wolves + num_bushes */
 #define WAB2_MAX_OSTRICHES 8
 #define WAB2_MAX_SIDE 127     /* width, height (deltas are int8) */
+#define WAB2_MAX_POSITION (1 << 20) /* explicit reset positions (wab2_reset_at) */
+#define WAB2_MAX_RADIUS (1 << 20) /* view radii (a radius past the world's diagonal already sees all of it) */
 
 #define WAB2_OK 0
 #define WAB2_E_INVALID (-1)
@@ -94,7 +98,7 @@ typedef struct wab2_config {
   int32_t food_given_per_turn;         /* 5  (Bush.food_given_when_eaten), 0..255 */
   double wolf_starting_food;           /* 20 */
   double wolf_food_for_eating_ostrich; /* 10 */
-  int32_t lookout_view_radius;         /* 9, integer >= 0 */
+  int32_t lookout_view_radius;         /* 9, integer in [0, WAB2_MAX_RADIUS] */
   int32_t gatherer_view_radius;        /* 5 */
   int32_t wolf_view_radius;            /* 6 */
   /* ---- batched-surface extensions ---- */
@@ -130,11 +134,29 @@ typedef struct wab2_handle wab2_handle;
  * take_action before any reset_environment) or reset first as Env2Tests.py does. */
 int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t world_id_base,
                 int device, wab2_handle** out);
+
+/* wab2_create with caller-chosen positions: create_ostriches / create_wolves / create_bushes(n,
+ * spawn_positions) (WAB_Environment2.py:61-110).  positions: HOST int32 [B][N][2] (x, y) in
+ * entity-id order, or NULL (= wab2_create).  A pair with a negative coordinate takes the keyed
+ * random position of that entity (the reference fills a short spawn_positions list with random
+ * ones); otherwise it must be a tile of the world, [0, W) x [0, H) (World.create_* puts it in the
+ * frame as given, where the random path only ever draws tiles).  Synchronous. */
+int wab2_create_at(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t world_id_base,
+                   int device, const int32_t* positions, wab2_handle** out);
 int wab2_destroy(wab2_handle* h);
 int64_t wab2_batch(const wab2_handle* h);
 
 /* reset_environment() of all worlds, or of those with mask[b] != 0 (device u8 [B] or NULL). */
 int wab2_reset(wab2_handle* h, const uint8_t* mask, void* stream);
+
+/* reset_environment with caller-chosen positions: every entity's
+ * WAB_Environment2_Single.reset(new_x, new_y) (WAB_Environment2_Single.py:36-41), then
+ * World.reset_world.  positions: HOST int32 [B][N][2] or NULL (= wab2_reset); a pair with a
+ * negative coordinate draws the random position (randint(0, W), randint(0, H), as the reference
+ * does for new_x < 0 or new_y < 0), others lie in [0, WAB2_MAX_POSITION]^2 (the entity's own,
+ * unbounded coordinates; its frame X/Y stay stale until it acts, as after any reset).  Entries
+ * of unmasked worlds are ignored.  Synchronises `stream` when positions != NULL. */
+int wab2_reset_at(wab2_handle* h, const uint8_t* mask, const int32_t* positions, void* stream);
 
 /* One turn of every world.  actions [B][N] int8 (any value: those outside an entity's act
  * branches are no-ops, as in World.py:25-81); obs [B][N][R] records; reward [B][N] f32 (the

@@ -20,6 +20,9 @@ def _lib():
         L.wabt_create.argtypes = [P, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64]
         L.wabt_destroy.argtypes = [P]
         L.wabt_reset.argtypes = [P, P]
+        L.wabt_create_at.restype = P
+        L.wabt_create_at.argtypes = [P, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64, P]
+        L.wabt_reset_at.argtypes = [P, P, P]
         L.wabt_step.argtypes = [P] * 6 + [ctypes.c_int]
         L.wabt_get_state.argtypes = [P] * 8
         L.wabt_record_size.argtypes = [P]
@@ -31,7 +34,8 @@ class OracleTorus:
     """B torus worlds on the host CPU, same array layouts as wab_torus.h."""
 
     def __init__(self, width=32, height=32, num_ostriches=1, num_wolves=8, num_bushes=16,
-                 game_options=None, batch=1, seed=0x5EED, world_id_base=0, autoreset=True):
+                 game_options=None, batch=1, seed=0x5EED, world_id_base=0, autoreset=True,
+                 spawn_positions=None):
         from wab_gym_amd.torus_options import make_config  # config translation only
 
         self.cfg, self.options = make_config(width, height, num_ostriches, num_wolves, num_bushes,
@@ -40,7 +44,8 @@ class OracleTorus:
         self.NO, self.NW, self.NB = int(num_ostriches), int(num_wolves), int(num_bushes)
         self.N = self.NO + self.NW + self.NB
         self.R = int(_lib().wabt_record_size(ctypes.addressof(self.cfg)))
-        self.h = _lib().wabt_create(ctypes.addressof(self.cfg), self.B, seed, world_id_base)
+        pos = None if spawn_positions is None else self._positions(spawn_positions)
+        self.h = _lib().wabt_create_at(ctypes.addressof(self.cfg), self.B, seed, world_id_base, _p(pos))
         self.records = np.zeros((self.B, self.N, self.R), np.uint8)
         self.reward = np.zeros((self.B, self.N), np.float32)
         self.done = np.zeros((self.B, self.N), np.uint8)
@@ -51,9 +56,19 @@ class OracleTorus:
             _lib().wabt_destroy(self.h)
             self.h = None
 
-    def reset(self, mask=None):
+    def _positions(self, pos):
+        """[N, 2] (every world alike) or [B, N, 2] int32 positions (negative: random)."""
+        a = np.asarray(pos, dtype=np.int32)
+        if a.shape == (self.N, 2):
+            a = np.broadcast_to(a, (self.B, self.N, 2))
+        if a.shape != (self.B, self.N, 2):
+            raise ValueError("positions must have shape (%d, 2) or (%d, %d, 2)" % (self.N, self.B, self.N))
+        return np.ascontiguousarray(a)
+
+    def reset(self, mask=None, positions=None):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
-        _lib().wabt_reset(self.h, _p(m))
+        pos = None if positions is None else self._positions(positions)
+        _lib().wabt_reset_at(self.h, _p(m), _p(pos))
 
     def step(self, actions, nthreads=1):
         a = np.ascontiguousarray(actions, dtype=np.int8).reshape(self.B, self.N)

@@ -78,7 +78,26 @@ static void reset_object(const wabt* w, wabt_entity* en, int type, int64_t x, in
   }
 }
 
+/* an explicit position of entity i in world b (pos [B][N][2] or NULL), or 0: the keyed draw
+ * (a negative coordinate: WAB_Environment2_Single.reset's `new_x < 0 or new_y < 0`, :38) */
+static int explicit_pos(const wabt* w, const int32_t* pos, int64_t b, int64_t i, int64_t* x, int64_t* y) {
+  if (!pos) return 0;
+  const int32_t* q = pos + (b * w->N + i) * 2;
+  if (q[0] < 0 || q[1] < 0) return 0;
+  *x = q[0];
+  *y = q[1];
+  return 1;
+}
+
+void* wabt_create_at(const wab2_config* cfg, int64_t B, uint64_t seed, int64_t base, const int32_t* pos);
+
 void* wabt_create(const wab2_config* cfg, int64_t B, uint64_t seed, int64_t base) {
+  return wabt_create_at(cfg, B, seed, base, NULL);
+}
+
+/* create_*(n, spawn_positions) (WAB_Environment2.py:61-110): the given positions, the random
+ * ones where a pair is negative */
+void* wabt_create_at(const wab2_config* cfg, int64_t B, uint64_t seed, int64_t base, const int32_t* pos) {
   wabt* w = (wabt*)calloc(1, sizeof(wabt));
   w->cfg = *cfg;
   w->B = B;
@@ -98,8 +117,11 @@ void* wabt_create(const wab2_config* cfg, int64_t B, uint64_t seed, int64_t base
     const uint64_t ek = wabo_episode_key(seed, (uint64_t)(base + b), 0);
     for (int64_t i = 0; i < w->N; ++i) {
       wabt_entity* en = &w->e[b * w->N + i];
-      const int64_t x = randint_keyed(ek, SITE_T_CREATE, 0, i, 0, 0, cfg->width - 1);
-      const int64_t y = randint_keyed(ek, SITE_T_CREATE, 0, i, 1, 0, cfg->height - 1);
+      int64_t x, y;
+      if (!explicit_pos(w, pos, b, i, &x, &y)) {
+        x = randint_keyed(ek, SITE_T_CREATE, 0, i, 0, 0, cfg->width - 1);
+        y = randint_keyed(ek, SITE_T_CREATE, 0, i, 1, 0, cfg->height - 1);
+      }
       reset_object(w, en, type_of(w, i), x, y);
       en->X = x;
       en->Y = y;
@@ -120,24 +142,29 @@ void wabt_destroy(void* h) {
 /* reset_environment (WAB_Environment2.py:113-118): every entity's reset() with
  * _get_random_spawn_indices (randint(0, W), randint(0, H): both ends included), then
  * reset_world (World.py:350-358): Visible = True; its X/Y assignments write a copy (no-op) */
-static void reset_world(wabt* w, int64_t b) {
+static void reset_world(wabt* w, int64_t b, const int32_t* pos) {
   const int64_t ep = ++w->episode[b];
   const uint64_t ek = wabo_episode_key(w->seed, (uint64_t)(w->base + b), (uint64_t)ep);
   for (int64_t i = 0; i < w->N; ++i) {
     wabt_entity* en = &w->e[b * w->N + i];
-    const int64_t x = randint_keyed(ek, SITE_T_RESET, 0, i, 0, 0, w->cfg.width);
-    const int64_t y = randint_keyed(ek, SITE_T_RESET, 0, i, 1, 0, w->cfg.height);
+    int64_t x, y;
+    if (!explicit_pos(w, pos, b, i, &x, &y)) {  /* reset(new_x, new_y), WAB_Environment2_Single.py:36-41 */
+      x = randint_keyed(ek, SITE_T_RESET, 0, i, 0, 0, w->cfg.width);
+      y = randint_keyed(ek, SITE_T_RESET, 0, i, 1, 0, w->cfg.height);
+    }
     reset_object(w, en, type_of(w, i), x, y);
     en->visible = 1;
   }
   w->turn[b] = 0;
 }
 
-void wabt_reset(void* h, const uint8_t* mask) {
+void wabt_reset_at(void* h, const uint8_t* mask, const int32_t* pos) {
   wabt* w = (wabt*)h;
   for (int64_t b = 0; b < w->B; ++b)
-    if (!mask || mask[b]) reset_world(w, b);
+    if (!mask || mask[b]) reset_world(w, b, pos);
 }
+
+void wabt_reset(void* h, const uint8_t* mask) { wabt_reset_at(h, mask, NULL); }
 
 /* min(a, c, key=abs): the first argument on a tie */
 static int64_t min_abs(int64_t a, int64_t c) { return llabs(c) < llabs(a) ? c : a; }
@@ -272,7 +299,7 @@ static void turn_world(wabt* w, int64_t b, const int8_t* act, uint8_t* rec, floa
     for (int64_t k = 0; k < w->NO; ++k) all_done &= w->e[b * w->N + k].status != 0;
     reset = all_done || (w->cfg.max_turns > 0 && w->turn[b] >= w->cfg.max_turns);
   }
-  if (reset) reset_world(w, b);
+  if (reset) reset_world(w, b, NULL);
   if (world_reset) *world_reset = (uint8_t)reset;
 }
 

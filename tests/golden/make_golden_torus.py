@@ -40,10 +40,20 @@ import torus_harness as th  # noqa: E402
 
 SEED = 0x5EED
 
+# the policy's knobs: an ostrich seeks the nearest visible bush when u < ostrich_bush, a wolf
+# chases the nearest visible ostrich with probability wolf_chase
+POLICY = {"ostrich_bush": 0.6, "wolf_chase": 0.55}
+# the hunt worlds of torus_c3: wolves always chase, the ostrich walks at random (kills, and
+# the kill-triggered early resets of the benched 1/8/16 instance)
+HUNT = {"ostrich_bush": 0.0, "wolf_chase": 1.0}
+
+
 SETS = {
     # name: (W, H, (n_ostriches, n_wolves, n_bushes), option overrides, world ids, turns, protocol)
     # BASELINE config 3's literal reading: 32x32 torus, 1 ostrich, 8 wolves, 16 bushes
-    "torus_c3": (32, 32, (1, 8, 16), {}, list(range(8)) + [65535, 2**33 + 7], 170, "autoreset"),
+    # (+ six hunt worlds 400-405, policy HUNT: kills and kill-triggered early resets at 1/8/16)
+    "torus_c3": (32, 32, (1, 8, 16), {}, list(range(8)) + [65535, 2**33 + 7] + list(range(400, 406)), 170,
+                 "autoreset"),
     # several ostriches (eat order, the Visible-label quirk of World.py:115), a rectangular
     # world whose lookout radius reaches past the middle (both wrap branches), bushes that run
     # dry through take_food's second branch (12 -> 7 -> 2 -> 0)
@@ -61,7 +71,46 @@ SETS = {
                    list(range(200, 206)), 120, "autoreset"),
     # no resets: the world runs on after its ostrich is dead
     "torus_continue": (16, 16, (1, 3, 5), {}, list(range(300, 304)), 140, "continue"),
+    # caller-chosen positions: create_*(n, spawn_positions) and each entity's
+    # reset(new_x, new_y) (WAB_Environment2.py:61-110, WAB_Environment2_Single.py:36-41) at turns
+    # 0, 30 and 61, a quarter of them negative (the random position), some past the world's edge;
+    # the World_tests.py world size
+    "torus_placed": (20, 20, (2, 3, 4), {"lookout_view_radius": 10, "gatherer_view_radius": 8,
+                                         "wolf_view_radius": 6, "max_turns": 40},
+                     list(range(500, 504)), 90, "autoreset"),
 }
+# per-set extras: the hunt worlds' policy; the placed set's explicit resets (turn -> positions)
+POLICIES = {"torus_c3": {g: HUNT for g in range(400, 406)}}
+PLACED_RESETS = {"torus_placed": (0, 30, 61)}
+
+
+def placed_positions(e, W, H, N, k):
+    """The placed set's positions of world index e: k = -1 create (tiles of the world), k >= 0
+    the k-th explicit reset ((-1, -1) = random, x or y = W/H, beyond the edge, or a tile)."""
+    rng = np.random.RandomState(7000 + 97 * e + k)
+    if k < 0:
+        return np.stack([rng.randint(W, size=N), rng.randint(H, size=N)], -1).astype(np.int32)
+    out = np.zeros((N, 2), np.int32)
+    for i in range(N):
+        u = rng.random_sample()
+        if u < 0.25:
+            out[i] = (-1, -1) if rng.random_sample() < 0.5 else (-1 - rng.randint(3), rng.randint(H))
+        elif u < 0.4:
+            out[i] = (rng.choice([W, 2 * W + 3, 100]), rng.choice([H, rng.randint(H), 57]))
+        else:
+            out[i] = (rng.randint(W + 1), rng.randint(H + 1))
+    return out
+
+
+def reset_at(env, pos):
+    """reset_environment (WAB_Environment2.py:113-118) with each entity's reset(new_x, new_y)
+    (WAB_Environment2_Single.py:36-41) instead of its argument-less call: the same body, driving
+    the unmodified modules (the keyed episode counter as KeyedEnv2.reset_environment keeps it)."""
+    env._world._wab_episode += 1
+    for single, (x, y) in zip(env._environments, pos):
+        single.reset(int(x), int(y))
+    env.num_entities_acted_this_turn = 0
+    env._world.reset_world()
 
 JUNK = [-128, -1, 6, 7, 17, 127]
 
@@ -79,7 +128,7 @@ def _nearest(rec, off, types, want, rng):
     return best
 
 
-def choose_action(rng, kind, rec, off, types):
+def choose_action(rng, kind, rec, off, types, policy=POLICY):
     if rng.random_sample() < 0.03:
         return int(JUNK[rng.randint(len(JUNK))])
     if kind == "Bush":
@@ -88,11 +137,11 @@ def choose_action(rng, kind, rec, off, types):
         u = rng.random_sample()
         if u < 0.06:
             return int(4 + rng.randint(2))
-        tgt = _nearest(rec, off, types, "Bush", rng) if u < 0.6 else None
+        tgt = _nearest(rec, off, types, "Bush", rng) if u < policy["ostrich_bush"] else None
         if tgt is None:
             return int(rng.randint(6))
     else:
-        tgt = _nearest(rec, off, types, "Ostrich", rng) if rng.random_sample() < 0.55 else None
+        tgt = _nearest(rec, off, types, "Ostrich", rng) if rng.random_sample() < policy["wolf_chase"] else None
         if tgt is None:
             return int(rng.randint(5))
     _, dx, dy = tgt
@@ -126,23 +175,43 @@ def run_set(name):
         "create_df_xy": np.zeros((E, N, 2), np.int32),
         "reset0_obj_xy": np.zeros((E, N, 2), np.int32),
     }
+    placed = PLACED_RESETS.get(name)
+    if placed:
+        out["create_pos"] = np.zeros((E, N, 2), np.int32)
+        out["reset_pos"] = np.zeros((len(placed), E, N, 2), np.int32)
     t0 = time.time()
     kills = eats = resets = 0
     for e, g in enumerate(world_ids):
         rng = np.random.RandomState(5000 + e)
+        policy = POLICIES.get(name, {}).get(g, POLICY)
         env = th.make_env(SEED, g, W, H, opts)
-        env.create_ostriches(no)
-        env.create_wolves(nw)
-        env.create_bushes(nb)
+        if placed:
+            cp = placed_positions(e, W, H, N, -1)
+            out["create_pos"][e] = cp
+            env.create_ostriches(no, [tuple(map(int, p)) for p in cp[:no]])
+            env.create_wolves(nw, [tuple(map(int, p)) for p in cp[no:no + nw]])
+            env.create_bushes(nb, [tuple(map(int, p)) for p in cp[no + nw:]])
+        else:
+            env.create_ostriches(no)
+            env.create_wolves(nw)
+            env.create_bushes(nb)
         ents = env._world._entities
         out["create_df_xy"][e] = ents[["X", "Y"]].to_numpy(np.int64)
-        env.reset_environment()
+        if placed:
+            out["reset_pos"][0, e] = placed_positions(e, W, H, N, 0)
+            reset_at(env, out["reset_pos"][0, e])
+        else:
+            env.reset_environment()
         out["reset0_obj_xy"][e] = [(o.x, o.y) for o in ents["Entity_Object"]]
         for t in range(T):
+            if placed and t in placed[1:]:
+                k = placed.index(t)
+                out["reset_pos"][k, e] = placed_positions(e, W, H, N, k)
+                reset_at(env, out["reset_pos"][k, e])
             for i in range(N):
                 rec = out["records"][t, e, i]
                 th.encode_obs(env.get_obs(i), i, types, nb, rec)
-                a = choose_action(rng, types[i], rec, off, types)
+                a = choose_action(rng, types[i], rec, off, types, policy)
                 out["actions"][t, e, i] = a
                 r, d = env.take_action(i, a)
                 out["reward"][t, e, i] = float(r)
@@ -164,6 +233,8 @@ def run_set(name):
     meta = {"set": name, "seed": SEED, "world_ids": [int(g) for g in world_ids], "T": T,
             "protocol": protocol, "width": W, "height": H, "num_ostriches": no, "num_wolves": nw,
             "num_bushes": nb, "record_size": R, "options": full,
+            "hunt_worlds": sorted(int(g) for g in POLICIES.get(name, {})),
+            "placed_resets": list(placed) if placed else [],
             "generator": "tests/golden/make_golden_torus.py",
             "reference": "Environment 2.0/WAB_Environment2.py + World.py (johnmatthewtennant/wab-gym) "
                          "under the keyed random of tests/golden/torus_harness.py",

@@ -39,6 +39,30 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_product_library_is_not_a_diagnostic_build():
+    """csrc/wab_build_guard.h: the product build refuses the diagnostic macros, a diagnostic
+    build must say so, and the product library does not export wab_diagnostic_build."""
+    guard = os.path.join(REPO, "wab_gym_amd", "csrc", "wab_build_guard.h")
+
+    def compiles(*defs):
+        r = subprocess.run(["g++", "-fsyntax-only", "-x", "c++", "-include", guard, "-"] + list(defs),
+                           input="int main() { return 0; }\n", capture_output=True, text=True)
+        return r.returncode == 0
+
+    assert compiles("-DWAB_PRODUCT_BUILD")
+    for macro in ("WAB_STAMPS", "WAB2_STAMPS", "WAB_ROLL_FLOOR=1", "WAB_WIDE_ROLL_FLOOR=1",
+                  "WAB2_ABLATE=2", "WAB_ONLY_WAVE=0"):
+        assert not compiles("-DWAB_PRODUCT_BUILD", "-D" + macro), macro
+        assert not compiles("-D" + macro), macro
+        assert not compiles("-DWAB_PRODUCT_BUILD", "-DWAB_DIAGNOSTIC_BUILD", "-D" + macro), macro
+        assert compiles("-DWAB_DIAGNOSTIC_BUILD", "-D" + macro), macro
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libwab_hip.so not built")
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "wab_diagnostic_build" not in out
+
+
 def test_library_loads_and_reports_abi():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libwab_hip.so not built")
@@ -149,3 +173,10 @@ def test_torus_record_size_and_validation_on_host():
     assert b"ostriches" in L.wab2_last_error()
     cfg.num_ostriches, cfg.width = 1, 128
     assert L.wab2_record_size(ctypes.addressof(cfg)) == -1
+    cfg.width = 32
+    for f in ("lookout_view_radius", "gatherer_view_radius", "wolf_view_radius"):
+        setattr(cfg, f, (1 << 20) + 1)  # C callers get the host wrapper's cap too (int32 view math)
+        assert L.wab2_record_size(ctypes.addressof(cfg)) == -1, f
+        assert b"radii" in L.wab2_last_error()
+        setattr(cfg, f, 1 << 20)
+        assert L.wab2_record_size(ctypes.addressof(cfg)) == 96, f

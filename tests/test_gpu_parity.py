@@ -1114,3 +1114,51 @@ def test_wide_step_into_alternating_buffers():
         assert np.array_equal(env.done.cpu().numpy(), odone), t
     c = env.counters()
     assert c["wolf_overflow"] == 0 and c["handoff_timeouts"] == 0 and c["steps"] == 120 * n
+
+
+def test_env_step_into_obs_ring_fresh_placement():
+    """BatchedWolvesAndBushesEnv(obs_placement="fresh") + step(actions, obs=slot): a closed
+    loop's ring of observation buffers on the wide view (the one-step rollout build) and on the
+    default view, against the oracle; every slot keeps its step's observation."""
+    import torch
+
+    for opts, stride, slots in (({"width": 31, "height": 31}, 32, 32), (None, 0, 8)):
+        n = 512
+        env = _env(opts, n, plane_stride=stride, wolf_slots=slots, obs_placement="fresh")
+        orc = _oracle(opts, n, stride=stride)
+        env.reset()
+        orc.reset()
+        ring = [env.alloc_obs() for _ in range(3)]
+        kept = []
+        rng = np.random.RandomState(5)
+        for t in range(40):
+            a = rng.randint(5, size=n)
+            obs, rew, done, _ = env.step(torch.as_tensor(a), obs=ring[t % 3])
+            op, of, orl, ost, orew, odone = orc.step(a, nthreads=16)
+            assert obs[0].data_ptr() == ring[t % 3]["planes"].data_ptr()
+            assert np.array_equal(ring[t % 3]["planes"].cpu().numpy(), op), t
+            assert np.array_equal(obs[3].cpu().numpy(), of), t
+            assert np.array_equal(rew.cpu().numpy(), orew), t
+            kept.append(op)
+            if t >= 2:  # the slot written two steps ago still holds its step
+                assert np.array_equal(ring[(t - 2) % 3]["planes"].cpu().numpy(), kept[t - 2]), t
+        with pytest.raises(RuntimeError):
+            env.render(scale=1)  # the env's own buffer was not written
+        with pytest.raises(ValueError):
+            env.step(torch.zeros(n, dtype=torch.int8), obs={"planes": ring[0]["planes"][:, :, :, :1],
+                                                           "scalars": ring[0]["scalars"]})
+        env.close()
+
+
+def test_rollout_updates_obs_views_eagerly():
+    """After env.rollout(T), the obs tuple an earlier step() returned shows step T-1 in planes and
+    scalars alike (planes[T-1] copied into the env's buffer on the launch's stream)."""
+    import torch
+
+    env = _env(None, 256)
+    env.reset()
+    obs, _, _, _ = env.step(torch.zeros(256, dtype=torch.int8))
+    planes, scal, rew, done = env.rollout(torch.randint(0, 5, (9, 256), device="cuda:0"))
+    for k in range(3):
+        assert torch.equal(obs[k], planes[8, :, k, :, :env.H])
+    assert torch.equal(obs[3], scal[8, 0]) and torch.equal(obs[5], scal[8, 2])

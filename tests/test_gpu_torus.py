@@ -15,7 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SETS = ["torus_c3", "torus_multi", "torus_tiny", "torus_continue"]
+SETS = ["torus_c3", "torus_multi", "torus_tiny", "torus_continue", "torus_placed"]
 
 
 def load_set(name):
@@ -41,6 +41,15 @@ def oracle(meta, base, batch, autoreset=None):
                        world_id_base=base, autoreset=ar)
 
 
+def placed_schedule(d, meta, e):
+    """A placed set's explicit positions of world index e: (create [N, 2] or None, {turn:
+    reset positions [N, 2]}; turn 0 is the first reset)."""
+    turns = meta.get("placed_resets") or []
+    if not turns:
+        return None, {}
+    return d["create_pos"][e], {t: d["reset_pos"][k, e] for k, t in enumerate(turns)}
+
+
 def check_state(env, d, t, e, where):
     s = env.state()
     NO = env.num_ostriches
@@ -57,12 +66,15 @@ def test_torus_steps_match_reference_golden(name):
 
     d, meta = load_set(name)
     for e, g in enumerate(meta["world_ids"]):
-        env = make_env(meta, g)
+        create, resets = placed_schedule(d, meta, e)
+        env = make_env(meta, g, spawn_positions=create)
         s = env.state()
         assert np.array_equal(s["df_xy"][0], d["create_df_xy"][e]), "create_* positions"
-        env.reset_environment()
+        env.reset_environment(positions=resets.get(0))
         assert np.array_equal(env.state()["obj_xy"][0], d["reset0_obj_xy"][e]), "reset positions"
         for t in range(meta["T"]):
+            if t > 0 and t in resets:
+                env.reset_environment(positions=resets[t])
             obs, rew, done, info = env.step(torch.as_tensor(d["actions"][t, e][None]))
             where = "%s world %d turn %d" % (name, g, t)
             o = obs[0].cpu().numpy()
@@ -83,9 +95,17 @@ def test_torus_rollout_matches_reference_golden(name):
     d, meta = load_set(name)
     T = meta["T"]
     for e, g in enumerate(meta["world_ids"]):
-        env = make_env(meta, g)
-        env.reset_environment()
-        obs, rew, done, wr = env.rollout(torch.as_tensor(d["actions"][:, e][:, None]))
+        create, resets = placed_schedule(d, meta, e)
+        env = make_env(meta, g, spawn_positions=create)
+        env.reset_environment(positions=resets.get(0))
+        # one launch per stretch between explicit resets (one launch for the sets without)
+        cuts = [0] + sorted(t for t in resets if t > 0) + [T]
+        parts = []
+        for t0, t1 in zip(cuts[:-1], cuts[1:]):
+            if t0 > 0:
+                env.reset_environment(positions=resets[t0])
+            parts.append(env.rollout(torch.as_tensor(d["actions"][t0:t1, e][:, None])))
+        obs, rew, done, wr = (torch.cat([p[k] for p in parts]) for k in range(4))
         o = obs[:, 0].cpu().numpy()
         bad = np.argwhere((o != d["records"][:, e]).any(axis=2))
         assert len(bad) == 0, "%s world %d: (turn, entity) %s differ" % (name, g, bad[:5].tolist())
@@ -303,3 +323,90 @@ def test_torus_rejects_bad_options():
                {"game_options": {"lookout_view_radius": 4.5}}):
         with pytest.raises(ValueError):
             BatchedWABEnvironment2(num_worlds=64, device="cuda:0", **kw)
+
+
+def _kat_env(W, H, counts, radius, positions):
+    from wab_gym_amd.torus import BatchedWABEnvironment2
+
+    opts = {"lookout_view_radius": radius, "gatherer_view_radius": radius}
+    return BatchedWABEnvironment2(W, H, opts, *counts, num_worlds=3, device="cuda:0",
+                                  spawn_positions=np.array(positions, np.int32))
+
+
+def test_torus_world_tests_no_wrap_kat_on_gpu():
+    """`Environment 2.0/World_tests.py:5-45` through the HIP kernel: a 20x20 world with the
+    test's six entities at the test's positions (wab2_create_at; ids in this surface's
+    ostrich, wolves, bushes order), the ostrich at (10, 10) looking with radius 8 sees all six at
+    the test's deltas, bushes with their 20 food."""
+    # ostrich (10, 10); wolves (5, 5), (15, 15); bushes (10, 5), (10, 10), (15, 10)
+    env = _kat_env(20, 20, (1, 2, 3), 8, [(10, 10), (5, 5), (15, 15), (10, 5), (10, 10), (15, 10)])
+    rec = env.get_obs(0)
+    for b in range(3):
+        rows, internal = env.frame(rec[b])
+        got = sorted((typ, dx, dy, tuple(extra)) for _, dx, dy, typ, extra in rows)
+        want = sorted([("Wolf", -5, -5, ()), ("Bush", 0, -5, (20,)), ("Ostrich", 0, 0, ()),
+                       ("Bush", 0, 0, (20,)), ("Bush", 5, 0, (20,)), ("Wolf", 5, 5, ())])
+        assert got == want, (b, rows)
+        assert internal[:2] == [10, 10]
+
+
+def test_torus_world_tests_wrap_kat_on_gpu():
+    """`World_tests.py:49-88` through the HIP kernel: the other ostrich (id 0 here) takes action 0
+    from (15, 15) to (15, 16) (wab2_take_action), then the ostrich at (19, 10) looking with
+    radius 10 (id 1) sees the wolf at x = 5 through the wrap (Delta_X 6) and the rows the
+    reference computes: the test's five plus the moved ostrich at (-4, 6) (World.py returns six
+    rows where the test asserts five: tests/test_torus_oracle.py)."""
+    import torch
+
+    # ostriches (15, 15) [the mover], (19, 10) [the observer]; wolves (5, 5), (15, 15);
+    # bushes (10, 10), (15, 10)
+    env = _kat_env(20, 20, (2, 2, 2), 10, [(15, 15), (19, 10), (5, 5), (15, 15), (10, 10), (15, 10)])
+    env.take_action(0, torch.zeros(3, dtype=torch.int8))
+    rec = env.get_obs(1)
+    for b in range(3):
+        rows, internal = env.frame(rec[b])
+        got = sorted((typ, dx, dy, tuple(extra)) for _, dx, dy, typ, extra in rows)
+        want = sorted([("Wolf", 6, -5, ()), ("Ostrich", 0, 0, ()), ("Bush", -9, 0, (20,)),
+                       ("Bush", -4, 0, (20,)), ("Wolf", -4, 5, ()), ("Ostrich", -4, 6, ())])
+        assert got == want, (b, rows)
+    assert env.state()["obj_xy"][0, 0].tolist() == [15, 16]
+
+
+def test_torus_explicit_positions_lockstep_vs_oracle():
+    """wab2_create_at / wab2_reset_at (explicit positions, a quarter of them negative = the
+    keyed random draw, reset positions up to 3 sides past the edge) at B = 4096, 1/8/16, against
+    the oracle given the same positions: full and masked resets, 60 turns, every record."""
+    import torch
+
+    from oracle.torus_oracle import OracleTorus
+    from wab_gym_amd.torus import BatchedWABEnvironment2
+
+    B, W, H, N = 4096, 32, 32, 25
+    rng = np.random.RandomState(11)
+    create = np.stack([rng.randint(W, size=(B, N)), rng.randint(H, size=(B, N))], -1).astype(np.int32)
+    create[rng.random_sample((B, N)) < 0.25] = -1
+    env = BatchedWABEnvironment2(W, H, None, 1, 8, 16, num_worlds=B, device="cuda:0", spawn_positions=create)
+    orc = OracleTorus(W, H, 1, 8, 16, batch=B, spawn_positions=create)
+    assert np.array_equal(env.state()["df_xy"], orc.state()["df_xy"])
+    hi = np.array([6] + [5] * 8 + [1] * 16)
+    for t in range(60):
+        if t % 20 == 0:
+            pos = np.stack([rng.randint(3 * W + 1, size=(B, N)), rng.randint(H + 1, size=(B, N))], -1)
+            pos[rng.random_sample((B, N)) < 0.25] = (-1, 5)
+            mask = None if t == 0 else (rng.random_sample(B) < 0.5).astype(np.uint8)
+            env.reset_environment(mask=mask, positions=pos.astype(np.int32))
+            orc.reset(mask=mask, positions=pos.astype(np.int32))
+            s_g, s_o = env.state(), orc.state()
+            for k in ("obj_xy", "df_xy", "food", "episode"):
+                assert np.array_equal(s_g[k], s_o[k]), (t, k)
+        a = (rng.randint(0, 1 << 20, size=(B, N)) % hi).astype(np.int8)
+        obs, rew, done, info = env.step(torch.as_tensor(a))
+        r_o, rw_o, d_o, wr_o = orc.step(a, nthreads=8)
+        assert np.array_equal(obs.cpu().numpy(), r_o), t
+        assert np.array_equal(rew.cpu().numpy(), rw_o), t
+        assert np.array_equal(info["world_reset"].cpu().numpy(), wr_o.astype(bool)), t
+    with pytest.raises(Exception):
+        BatchedWABEnvironment2(W, H, None, 1, 8, 16, num_worlds=2, device="cuda:0",
+                               spawn_positions=np.full((N, 2), W, np.int32))  # x = W is not a tile
+    with pytest.raises(Exception):
+        env.reset_environment(positions=np.full((N, 2), (1 << 20) + 1, np.int64))

@@ -12,7 +12,7 @@ import pytest
 from oracle.torus_oracle import OracleTorus
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SETS = ["torus_c3", "torus_multi", "torus_tiny", "torus_continue"]
+SETS = ["torus_c3", "torus_multi", "torus_tiny", "torus_continue", "torus_placed"]
 
 
 def load_set(name):
@@ -21,10 +21,20 @@ def load_set(name):
     return d, meta
 
 
-def oracle_for(meta, world_id, batch=1):
+def oracle_for(meta, world_id, batch=1, spawn_positions=None):
     return OracleTorus(meta["width"], meta["height"], meta["num_ostriches"], meta["num_wolves"],
                        meta["num_bushes"], meta["options"], batch=batch, seed=meta["seed"],
-                       world_id_base=world_id, autoreset=meta["protocol"] == "autoreset")
+                       world_id_base=world_id, autoreset=meta["protocol"] == "autoreset",
+                       spawn_positions=spawn_positions)
+
+
+def placed_schedule(d, meta, e):
+    """The explicit positions of world index e of a placed set: (create [N, 2] or None,
+    {turn: reset positions [N, 2]}; turn 0 is the first reset)."""
+    turns = meta.get("placed_resets") or []
+    if not turns:
+        return None, {}
+    return d["create_pos"][e], {t: d["reset_pos"][k, e] for k, t in enumerate(turns)}
 
 
 @pytest.mark.parametrize("name", SETS)
@@ -32,13 +42,16 @@ def test_oracle_reproduces_reference(name):
     d, meta = load_set(name)
     T, NO = meta["T"], meta["num_ostriches"]
     for e, g in enumerate(meta["world_ids"]):
-        o = oracle_for(meta, g)
+        create, resets = placed_schedule(d, meta, e)
+        o = oracle_for(meta, g, spawn_positions=create)
         s = o.state()
         assert np.array_equal(s["df_xy"][0], d["create_df_xy"][e]), "create_* positions"
-        o.reset()
+        o.reset(positions=resets.get(0))
         s = o.state()
         assert np.array_equal(s["obj_xy"][0], d["reset0_obj_xy"][e]), "reset_environment positions"
         for t in range(T):
+            if t > 0 and t in resets:
+                o.reset(positions=resets[t])
             rec, rew, done, wr = o.step(d["actions"][t, e][None])
             where = "%s world %d turn %d" % (name, g, t)
             bad = np.nonzero((rec[0] != d["records"][t, e]).any(axis=1))[0]
@@ -54,10 +67,62 @@ def test_oracle_reproduces_reference(name):
             assert np.array_equal(s["status"][0, :NO], d["status"][t, e, :NO]), where + " status"
 
 
+def wrapped_rows(d, meta):
+    """Visible rows whose (Delta_X, Delta_Y) is not the plain difference of the frame positions
+    the observer saw (World.py:255-291 replaced it through the wrap), and a check of each: the
+    frame X/Y at observation time are df_xy[t] for the entities that acted before the observer
+    this turn and the previous turn's (create_df_xy at t = 0) for the others and itself; a reset
+    leaves the frame as it was (World.py:355-356).  Every visible row's delta must equal the plain
+    one per axis or differ from it by the side (W or H), and be strictly shorter when it does."""
+    W, H = meta["width"], meta["height"]
+    rec = d["records"]
+    T, E, N = rec.shape[:3]
+    prev = np.concatenate([d["create_df_xy"][None], d["df_xy"][:-1]], 0).astype(np.int64)
+    cur = d["df_xy"].astype(np.int64)
+    i_idx = np.arange(N)[:, None]
+    j_idx = np.arange(N)[None, :]
+    # position of j as observer i saw it: [T, E, i, j, 2]
+    pos = np.where((j_idx < i_idx)[None, None, :, :, None], cur[:, :, None, :, :], prev[:, :, None, :, :])
+    me = prev[:, :, :, None, :]
+    plain = pos - me
+    vis = (rec[..., 16:20].copy().view(np.uint32)[..., 0][..., None] >> j_idx.astype(np.uint32)) & 1
+    vis = vis.astype(bool)
+    dl = rec[..., 24:24 + 2 * N].view(np.int8).astype(np.int64).reshape(T, E, N, N, 2)
+    side = np.array([W, H])
+    ok_axis = (dl == plain) | ((np.abs(dl - plain) == side) & (np.abs(dl) < np.abs(plain)))
+    assert ok_axis.all(-1)[vis].all(), "a visible delta is neither plain nor a shorter wrap"
+    return int(((dl != plain).any(-1) & vis).sum())
+
+
+def early_resets(d, meta):
+    """World resets before max_turns turns of an episode: with one ostrich and no ostrich hunger,
+    each is a kill (the kill, its loc[j] label quirk and the reset in one turn)."""
+    wr = d["world_reset"]
+    n = 0
+    for e in range(wr.shape[1]):
+        ep_len = 0
+        for t in range(wr.shape[0]):
+            ep_len += 1
+            if wr[t, e]:
+                n += ep_len < meta["options"]["max_turns"]
+                ep_len = 0
+    return n
+
+
 def test_golden_sets_exercise_the_quirks():
     """The fixtures hold what the parity claims rest on: kills, eats, resets, stale frame
     positions after a reset, emptied bushes still eaten, wrapped deltas, x = W spawns."""
     seen = dict(kill=0, eat=0, reset=0, stale=0, wrapped=0, x_eq_w=0, empty_eat=0, label_quirk=0)
+    for name in SETS:
+        d, meta = load_set(name)
+        # every set's view rule is exercised through the wrap, each of its rows checked
+        w = wrapped_rows(d, meta)
+        assert w >= 500, (name, w)
+        seen["wrapped"] += w
+    # the benched 1/8/16 set (torus_c3, the wab_torus_kernel<7, 1, 8, 16> instance): kills, each
+    # ending its episode early (the hunt worlds, wolves chasing)
+    d, meta = load_set("torus_c3")
+    assert early_resets(d, meta) >= 20, early_resets(d, meta)
     for name in SETS:
         d, meta = load_set(name)
         W, H, N, NB, NO = meta["width"], meta["height"], d["records"].shape[2], meta["num_bushes"], meta["num_ostriches"]
@@ -68,17 +133,13 @@ def test_golden_sets_exercise_the_quirks():
         seen["x_eq_w"] += int((d["reset0_obj_xy"][..., 0] == W).sum() + (d["obj_xy"][..., 0] == W).sum())
         obj_mod = np.stack([d["obj_xy"][..., 0] % W, d["obj_xy"][..., 1] % H], -1)
         seen["stale"] += int((obj_mod != d["df_xy"]).any(-1).sum())
-        dl = d["records"][..., 24:24 + 2 * N].view(np.int8).astype(int)
-        seen["wrapped"] += int(((np.abs(dl[..., 0::2]) > W // 2) | (np.abs(dl[..., 1::2]) > H // 2)).sum())
         bf = d["food"][..., N - NB:]
         seen["empty_eat"] += int((bf == 0).sum())
         vis, st = d["visible"][..., :NO], d["status"][..., :NO]
         seen["label_quirk"] += int(((st == 2) & vis).sum())
     assert seen["kill"] > 20 and seen["eat"] > 50 and seen["reset"] > 20, seen
     assert seen["stale"] > 100 and seen["x_eq_w"] > 0 and seen["empty_eat"] > 0, seen
-    # wrapped deltas are at most half a side by construction; the count above finds none of
-    # those wider ones, which is itself a check of the one-sided wrap rule
-    assert seen["wrapped"] >= 0
+    assert seen["wrapped"] > 10000, seen
     assert seen["label_quirk"] > 0, seen
 
 

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B the variant libraries: bench default, two rounds
+export WAB_DIAGNOSTIC_OK=1  # variant libraries (tools/build_variants.sh) are diagnostic builds
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab

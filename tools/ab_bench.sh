@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B variant libraries (wab_gym_amd/_lib/var/lib_<v>.so) on one bench config, two rounds:
 #   tools/ab_bench.sh CONFIG v1 v2 ...   (prints us/step of the line and of the per-step launches)
+export WAB_DIAGNOSTIC_OK=1  # variant libraries (tools/build_variants.sh) are diagnostic builds
 set -e
 export TMPDIR=/tmp
 cfg=$1; shift

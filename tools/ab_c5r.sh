@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B variant libraries on the C5 rollout bench (wab_rollout_features, T = 32): us per step
+export WAB_DIAGNOSTIC_OK=1  # variant libraries (tools/build_variants.sh) are diagnostic builds
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab_c5r

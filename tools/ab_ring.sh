@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B variant libraries on the per-step wide31 line into a 32-slot obs ring, two rounds:
 #   tools/ab_ring.sh v1 v2 ...
+export WAB_DIAGNOSTIC_OK=1  # variant libraries (tools/build_variants.sh) are diagnostic builds
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab_ring

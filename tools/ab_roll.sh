@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B variant libraries on the rollout bench (T = 32): tools/ab_roll.sh v1 v2 ...
+export WAB_DIAGNOSTIC_OK=1  # variant libraries (tools/build_variants.sh) are diagnostic builds
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab_roll

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B the torus variant libraries (tools/build_variants.sh with VARIANT_SRC=wab_torus):
 #   tools/ab_torus.sh OUT_DIR variant ...   (bench.py --config torus, two rounds each)
+export WAB_DIAGNOSTIC_OK=1  # variant libraries (tools/build_variants.sh) are diagnostic builds
 set -e
 export TMPDIR=/tmp
 out=$1; shift

@@ -5,7 +5,7 @@ set -e
 REPO=$(cd "$(dirname "$0")/.." && pwd)
 C=$REPO/wab_gym_amd/csrc
 O=/tmp/wab_variants
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Werror"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Werror -DWAB_DIAGNOSTIC_BUILD"  # never the product library (wab_build_guard.h)
 mkdir -p $O $REPO/wab_gym_amd/_lib/var
 VAR=${VARIANT_SRC:-wab_step_small}   # the source compiled per variant; the others once
 ALL="wab_step wab_step_small wab_step_wide wab_features wab_render wab_egocentric wab_torus wab_capi"

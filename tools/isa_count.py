@@ -18,7 +18,7 @@ KERNEL = os.environ.get("ISA_KERNEL", "_ZN3wab14wab_step_smallILi8ELi11ELb0ELb0E
 
 def counts(flags):
     out = "/tmp/isa_count.s"
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-DWAB_DIAGNOSTIC_BUILD",
                            "--cuda-device-only", "-S", SRC, "-o", out] + flags, stderr=subprocess.DEVNULL)
     s = open(out).read()
     a = s.index(KERNEL + ":")

@@ -39,10 +39,11 @@ def main():
 
     if not args.no_build:
         src = [os.path.join(ge.CSRC, s) for s in ge.HIP_SOURCES]
-        subprocess.run([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DWAB_STAMPS"] + args.cflags.split()
+        subprocess.run([ge._hipcc()] + [f for f in ge.HIPCC_FLAGS if f != "-DWAB_PRODUCT_BUILD"] + ["-DWAB_STAMPS", "-DWAB_DIAGNOSTIC_BUILD"] + args.cflags.split()
                        + ["-o", args.out] + src, check=True)
     if args.build_only:
         return
+    os.environ["WAB_DIAGNOSTIC_OK"] = "1"
     os.environ["WAB_LIB"] = args.lib if args.no_build else OUT
     import numpy as np
     import torch

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--lib", default="wab_gym_amd/_lib/var/lib_st.so")
     ap.add_argument("--batch", type=int, default=65536)
     args = ap.parse_args()
+    os.environ["WAB_DIAGNOSTIC_OK"] = "1"
     os.environ["WAB_LIB"] = args.lib
     import ctypes
 

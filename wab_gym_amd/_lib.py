@@ -22,7 +22,7 @@ EXPORTED = [
     # include/wab_torus.h: the Environment 2.0 torus world
     "wab2_abi_version", "wab2_last_error", "wab2_record_size", "wab2_create", "wab2_destroy",
     "wab2_batch", "wab2_reset", "wab2_step", "wab2_rollout", "wab2_get_state", "wab2_get_counters",
-    "wab2_get_obs", "wab2_take_action",
+    "wab2_get_obs", "wab2_take_action", "wab2_create_at", "wab2_reset_at",
 ]
 
 ABI2_VERSION = 1
@@ -64,6 +64,10 @@ def load():
     except ImportError:
         pass
     L = ctypes.CDLL(LIB_PATH)
+    if hasattr(L, "wab_diagnostic_build") and os.environ.get("WAB_DIAGNOSTIC_OK") != "1":
+        # a stamps / store-floor / ablation build (csrc/wab_build_guard.h): results wrong by design
+        raise WabError("%s is a diagnostic build (wab_diagnostic_build); the product library is "
+                       "wab_gym_amd/_lib/libwab_hip.so (set WAB_DIAGNOSTIC_OK=1 only in tools/)" % LIB_PATH)
     P, I64, U64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32
     L.wab_abi_version.restype = ctypes.c_int
     L.wab_last_error.restype = ctypes.c_char_p
@@ -101,6 +105,8 @@ def load():
     L.wab2_batch.argtypes = [P]
     L.wab2_batch.restype = I64
     L.wab2_reset.argtypes = [P, P, P]
+    L.wab2_create_at.argtypes = [P, I64, U64, I64, ctypes.c_int, P, ctypes.POINTER(P)]
+    L.wab2_reset_at.argtypes = [P, P, P, P]
     L.wab2_step.argtypes = [P, P, P, P, P, P, P]
     L.wab2_rollout.argtypes = [P, P, I32, P, P, P, P, P]
     L.wab2_get_state.argtypes = [P] * 9

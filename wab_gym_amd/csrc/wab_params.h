@@ -4,6 +4,8 @@
 // (include/wab.h) and passed by value as the kernel argument (scalar-loaded).
 #pragma once
 
+#include "wab_build_guard.h"
+
 #include <stdint.h>
 
 namespace wab {

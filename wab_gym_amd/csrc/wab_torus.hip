@@ -31,6 +31,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -102,6 +104,7 @@ struct TParams {
   uint8_t* done;          // [T][B][N]
   uint8_t* world_reset;   // [T][B] or null
   const uint8_t* mask;    // reset kernel: [B] or null
+  const int32_t* pos;     // create / reset kernels: explicit positions [B][N][2] or null
   int64_t B, Bp, world_base;
   uint64_t seed;
   int32_t T, N, NO, NW, NB, NM, R, W, H;
@@ -1053,15 +1056,31 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
 #undef WAB2_PHASE_PARAMS
 }
 
-// create_ostriches / create_wolves / create_bushes with random positions: randint(0, W - 1),
-// randint(0, H - 1) per entity (WAB_Environment2.py:64-106), episode 0; one lane per world
+// an explicit position of entity e in world g (wab2_create_at / wab2_reset_at), or false: the
+// keyed random draw (a negative coordinate asks for it, as WAB_Environment2_Single.reset's
+// `new_x < 0 or new_y < 0` does, WAB_Environment2_Single.py:36-41)
+__device__ __forceinline__ bool explicit_pos(const TParams& p, int64_t g, int e, int& x, int& y) {
+  if (!p.pos || g >= p.B) return false;
+  const int32_t* q = p.pos + (g * p.N + e) * 2;
+  if (q[0] < 0 || q[1] < 0) return false;
+  x = q[0];
+  y = q[1];
+  return true;
+}
+
+// create_ostriches / create_wolves / create_bushes: spawn_positions given, or random positions
+// randint(0, W - 1), randint(0, H - 1) per entity (WAB_Environment2.py:61-110), episode 0; one
+// lane per world
 __global__ void wab_torus_create_kernel(TParams p) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= p.Bp) return;
   const uint64_t ek = world_key(p, g, 0);
   for (int e = 0; e < p.N; ++e) {
-    const int x = keyed_below(ek, SITE_T_CREATE, 0, e, 0, (uint32_t)p.W);
-    const int y = keyed_below(ek, SITE_T_CREATE, 0, e, 1, (uint32_t)p.H);
+    int x, y;
+    if (!explicit_pos(p, g, e, x, y)) {
+      x = keyed_below(ek, SITE_T_CREATE, 0, e, 0, (uint32_t)p.W);
+      y = keyed_below(ek, SITE_T_CREATE, 0, e, 1, (uint32_t)p.H);
+    }
     const int64_t a = (int64_t)e * p.Bp + g;
     p.ox[a] = x;
     p.oy[a] = y;
@@ -1074,15 +1093,20 @@ __global__ void wab_torus_create_kernel(TParams p) {
   p.episode[g] = 0;
 }
 
-// reset_environment (WAB_Environment2.py:113-118) of the masked worlds; one lane per world
+// reset_environment (WAB_Environment2.py:113-118) of the masked worlds, each entity's
+// reset(new_x, new_y) with the given position or the random one (WAB_Environment2_Single.py:36-48);
+// one lane per world
 __global__ void wab_torus_reset_kernel(TParams p) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= p.B || (p.mask && !p.mask[g])) return;
   const uint32_t ep = p.episode[g] + 1u;
   const uint64_t ek = world_key(p, g, ep);
   for (int e = 0; e < p.N; ++e) {
-    const int x = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)p.W + 1u);
-    const int y = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)p.H + 1u);
+    int x, y;
+    if (!explicit_pos(p, g, e, x, y)) {
+      x = keyed_below(ek, SITE_T_RESET, 0, e, 0, (uint32_t)p.W + 1u);
+      y = keyed_below(ek, SITE_T_RESET, 0, e, 1, (uint32_t)p.H + 1u);
+    }
     const int64_t a = (int64_t)e * p.Bp + g;
     p.ox[a] = x;
     p.oy[a] = y;
@@ -1105,6 +1129,7 @@ struct wab2_handle {
   int device = 0;
   int n_blocks = 0;
   size_t lds = 0;
+  int32_t* pos = nullptr;  // device copy of the last explicit positions (wab2_create_at / wab2_reset_at)
   std::vector<void*> allocs;
 };
 
@@ -1152,9 +1177,28 @@ std::string validate(const wab2_config* c) {
   if (c->starting_role != 0 && c->starting_role != 1) return "starting_role must be 0 or 1";
   if (c->food_per_bush < 0 || c->food_per_bush > 255 || c->food_given_per_turn < 0 || c->food_given_per_turn > 255)
     return "food_per_bush and food_given_per_turn must be in [0, 255]";
-  if (c->lookout_view_radius < 0 || c->gatherer_view_radius < 0 || c->wolf_view_radius < 0)
-    return "view radii must be >= 0";
+  // (a radius past the world's diagonal sees everything; the cap keeps r - W + ex and W < ex + r
+  // of the view thresholds inside int32)
+  if (c->lookout_view_radius < 0 || c->gatherer_view_radius < 0 || c->wolf_view_radius < 0 ||
+      c->lookout_view_radius > WAB2_MAX_RADIUS || c->gatherer_view_radius > WAB2_MAX_RADIUS ||
+      c->wolf_view_radius > WAB2_MAX_RADIUS)
+    return "view radii must be in [0, 2^20]";
   if (c->max_turns < 0) return "max_turns must be >= 0";
+  return "";
+}
+
+// explicit positions [B][N][2] (host, or NULL): each pair either has a negative coordinate (the
+// keyed random draw) or lies in [0, xmax] x [0, ymax]
+std::string check_positions(const int32_t* pos, int64_t B, int N, int xmax, int ymax, const char* who) {
+  if (!pos) return "";
+  for (int64_t k = 0; k < B * N; ++k) {
+    const int32_t x = pos[2 * k], y = pos[2 * k + 1];
+    if (x < 0 || y < 0) continue;
+    if (x > xmax || y > ymax)
+      return std::string(who) + ": position (" + std::to_string(x) + ", " + std::to_string(y) + ") of world " +
+             std::to_string(k / N) + " entity " + std::to_string(k % N) + " outside [0, " + std::to_string(xmax) +
+             "] x [0, " + std::to_string(ymax) + "] (a negative coordinate draws the random position)";
+  }
   return "";
 }
 
@@ -1221,11 +1265,21 @@ int wab2_record_size(const wab2_config* cfg) {
 
 int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t world_id_base, int device,
                 wab2_handle** out) {
+  return wab2_create_at(cfg, batch, seed, world_id_base, device, nullptr, out);
+}
+
+int wab2_create_at(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t world_id_base, int device,
+                   const int32_t* positions, wab2_handle** out) {
   if (!out) return fail(WAB2_E_INVALID, "out is NULL");
   *out = nullptr;
   const std::string v = validate(cfg);
   if (!v.empty()) return fail(WAB2_E_INVALID, v);
   if (batch < 1) return fail(WAB2_E_INVALID, "batch must be >= 1");
+  const int N = cfg->num_ostriches + cfg->num_wolves + cfg->num_bushes;
+  // the frame holds create positions as they are (World.create_*, no modulo): on this surface
+  // they are tiles of the world, [0, W) x [0, H)
+  const std::string pv = check_positions(positions, batch, N, cfg->width - 1, cfg->height - 1, "wab2_create_at");
+  if (!pv.empty()) return fail(WAB2_E_INVALID, pv);
   DeviceGuard2 dg(device);
   wab2_handle* h = new wab2_handle();
   h->device = device;
@@ -1278,10 +1332,28 @@ int wab2_create(const wab2_config* cfg, int64_t batch, uint64_t seed, int64_t wo
   if (e == hipSuccess) { e = alloc(&q, NBp * 4); p.turn = (int32_t*)q; }
   if (e == hipSuccess) { e = alloc(&q, NBp * 4); p.episode = (uint32_t*)q; }
   if (e == hipSuccess) { e = alloc(&q, 2 * sizeof(unsigned long long)); p.counters = (unsigned long long*)q; }
-  if (e == hipSuccess && h->lds > 64 * 1024)
-    e = hipFuncSetAttribute(torus_kernel(p), hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+  if (e == hipSuccess && h->lds > 64 * 1024) {
+    // the attribute is per kernel instance, which handles of other bush counts share: only ever
+    // raise it (a later, smaller handle must not lower the limit an earlier one launches with)
+    static std::mutex mu;
+    static std::map<const void*, size_t> lds_set;
+    std::lock_guard<std::mutex> lock(mu);
+    size_t& cur = lds_set[torus_kernel(p)];
+    if (h->lds > cur) {
+      e = hipFuncSetAttribute(torus_kernel(p), hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds);
+      if (e == hipSuccess) cur = h->lds;
+    }
+  }
+  if (e == hipSuccess && positions) {
+    const size_t bytes = (size_t)batch * p.N * 2 * sizeof(int32_t);
+    e = alloc(&q, bytes);
+    h->pos = (int32_t*)q;
+    if (e == hipSuccess) e = hipMemcpy(h->pos, positions, bytes, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(wab2::wab_torus_create_kernel, dim3((unsigned)((p.Bp + 255) / 256)), dim3(256), 0, 0, p);
+    TParams pc = p;
+    pc.pos = h->pos;
+    hipLaunchKernelGGL(wab2::wab_torus_create_kernel, dim3((unsigned)((p.Bp + 255) / 256)), dim3(256), 0, 0, pc);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1306,17 +1378,37 @@ int wab2_destroy(wab2_handle* h) {
 int64_t wab2_batch(const wab2_handle* h) { return h ? h->p.B : 0; }
 
 int wab2_reset(wab2_handle* h, const uint8_t* mask, void* stream) {
+  return wab2_reset_at(h, mask, nullptr, stream);
+}
+
+int wab2_reset_at(wab2_handle* h, const uint8_t* mask, const int32_t* positions, void* stream) {
   if (!h) return fail(WAB2_E_INVALID, "handle is NULL");
   if (mask && h->next_entity != 0)
     return fail(WAB2_E_INVALID, "wab2_reset: a masked reset only between turns (entity " +
                                     std::to_string(h->next_entity) + " acts next)");
+  const TParams& hp = h->p;
+  const std::string pv = check_positions(positions, hp.B, hp.N, WAB2_MAX_POSITION, WAB2_MAX_POSITION, "wab2_reset_at");
+  if (!pv.empty()) return fail(WAB2_E_INVALID, pv);
   h->next_entity = 0;  // reset_environment: num_entities_acted_this_turn = 0 (WAB_Environment2.py:117)
   DeviceGuard2 dg(h->device);
   TParams p = h->p;
   p.mask = mask;
+  if (positions) {
+    // the handle's position buffer (the last reset_at's launch has finished: synchronised below)
+    const size_t bytes = (size_t)p.B * p.N * 2 * sizeof(int32_t);
+    if (!h->pos) {
+      void* q = nullptr;
+      HIP_TRY2(hipMalloc(&q, bytes));
+      h->allocs.push_back(q);
+      h->pos = (int32_t*)q;
+    }
+    HIP_TRY2(hipMemcpyAsync(h->pos, positions, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    p.pos = h->pos;
+  }
   hipLaunchKernelGGL(wab2::wab_torus_reset_kernel, dim3((unsigned)((p.B + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, p);
   HIP_TRY2(hipGetLastError());
+  if (positions) HIP_TRY2(hipStreamSynchronize((hipStream_t)stream));  // the host array may go now
   return WAB2_OK;
 }
 

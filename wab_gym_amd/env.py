@@ -45,7 +45,7 @@ class BatchedWolvesAndBushesEnv:
 
     def __init__(self, game_options=None, num_envs=4096, seed=0x5EED, device="cuda",
                  env_id_base=0, autoreset=True, return_terminal=False, plane_stride=0,
-                 wolf_slots=0, eaten_capacity=0, validate_actions=True):
+                 wolf_slots=0, eaten_capacity=0, validate_actions=True, obs_placement="same"):
         import torch
 
         self._torch = torch
@@ -78,6 +78,14 @@ class BatchedWolvesAndBushesEnv:
         _lib.check(lib.wab_create(ctypes.addressof(self.cfg), self.num_envs, self.base_seed,
                                   self.env_id_base, dev.index, ctypes.byref(h)), "wab_create")
         self._h = h
+        # which per-step build the wide (C3) kernel runs (wab_set_obs_placement, include/wab.h):
+        # "same" = every step into one buffer (the env's own: the per-step kernel), "fresh" = a
+        # closed loop stepping into a ring of buffers (step(actions, obs=...)): whole-line stores
+        if obs_placement not in ("same", "fresh"):
+            raise ValueError("obs_placement must be 'same' or 'fresh'")
+        self.obs_placement = obs_placement
+        _lib.check(lib.wab_set_obs_placement(h, _lib.OBS_FRESH_BUFFER if obs_placement == "fresh"
+                                             else _lib.OBS_SAME_BUFFER), "wab_set_obs_placement")
         B = self.num_envs
         u8 = dict(dtype=torch.uint8, device=dev)
         self._obs = self._alloc_obs()
@@ -89,7 +97,6 @@ class BatchedWolvesAndBushesEnv:
         self._zero_mask = torch.zeros((11, 11), **u8)
         self._reset_once = False
         self._planes_valid = True  # False while the obs planes buffer is stale (planes not stored)
-        self._pending_planes = None  # rollout()'s last-step planes, copied into _obs on first use
         self.n_actions = n_actions(opts)
         self.action_space = Discrete(self.n_actions)  # wab_env.py:188-191
         W, H = self.W, self.H
@@ -103,6 +110,12 @@ class BatchedWolvesAndBushesEnv:
                               reward_threshold=80)  # wab_env.py:140-146
 
     # ------------------------------------------------------------------ buffers
+    def alloc_obs(self):
+        """A new observation buffer (dict of planes [B,3,W,S] and scalars [3,B] u8) for
+        step(actions, obs=...), e.g. the slots of a closed loop's ring of observations."""
+        o = self._alloc_obs()
+        return {"planes": o["planes"], "scalars": o["scalars"]}
+
     def _alloc_obs(self):
         t = self._torch
         B = self.num_envs
@@ -153,7 +166,6 @@ class BatchedWolvesAndBushesEnv:
         if mask is not None:
             if not self._reset_once:
                 raise RuntimeError("the first reset must cover every env (mask=None)")
-            self._materialize_planes()  # (a masked reset rewrites only the masked envs' planes)
             m = t.as_tensor(mask, device=self.device).to(t.uint8).contiguous()
             if m.shape != (self.num_envs,):
                 raise ValueError("mask must have shape [num_envs]")
@@ -164,7 +176,6 @@ class BatchedWolvesAndBushesEnv:
         self._reset_once = True
         if m is None:
             self._planes_valid = True
-            self._pending_planes = None
         return self._obs_tuple(self._obs)
 
     def _step_actions(self, actions):
@@ -246,20 +257,30 @@ class BatchedWolvesAndBushesEnv:
         or None unless the env was made with return_terminal=True."""
         return self._term
 
-    def step(self, actions):
+    def step(self, actions, obs=None):
         """Advance every env one step (wab_env.py:250-342).  The returned obs, reward and done
-        are views of the env's buffers, overwritten by the next step (clone to keep them)."""
+        are views of the env's buffers, overwritten by the next step (clone to keep them).
+        obs=<dict from alloc_obs()> writes the observation into that buffer instead (a closed
+        loop keeping several steps' observations: construct with obs_placement="fresh"); the
+        returned obs are views of it, and the env's own buffer is not updated (render() and the
+        wrappers then need obs= too, until the next step()/reset() into the env's own)."""
         a = self._step_actions(actions)
         term = ctypes.addressof(self._term["struct"]) if self._term is not None else None
-        _lib.check(_lib.load().wab_step(self._h, a.data_ptr(), ctypes.addressof(self._obs["struct"]),
+        if obs is None:
+            st, keep, o = self._obs["struct"], None, self._obs
+        else:
+            if not (obs["planes"].is_contiguous() and obs["scalars"].is_contiguous()):
+                raise ValueError("obs= buffers must be contiguous (the step writes them in place)")
+            st, keep = self._obs_struct(obs)
+            o = {"planes": keep[0], "scalars": keep[1]}
+        _lib.check(_lib.load().wab_step(self._h, a.data_ptr(), ctypes.addressof(st),
                                         self.reward.data_ptr(), self.done.data_ptr(), term,
                                         self._stream()), "wab_step")
-        self._planes_valid = True
-        self._pending_planes = None
+        self._planes_valid = obs is None
         info = {}
         if self._term is not None:
             info["terminal_obs"] = self._obs_tuple(self._term)
-        return self._obs_tuple(self._obs), self.reward, self.done.view(self._torch.bool), info
+        return self._obs_tuple(o), self.reward, self.done.view(self._torch.bool), info
 
     def step_features(self, actions, features, store_planes=True):
         """step() fused with the PragmaticObsWrapper featurizer (wab_step_features): writes the
@@ -275,16 +296,15 @@ class BatchedWolvesAndBushesEnv:
                                                  features.data_ptr(), self._stream()),
                    "wab_step_features")
         self._planes_valid = bool(store_planes)
-        self._pending_planes = None
         return features, self.reward, self.done.view(self._torch.bool)
 
     def rollout(self, actions):
         """T fused steps: actions [T, B] -> (planes [T,B,3,W,S], scalars [T,3,B], reward [T,B],
         done [T,B]).  Equivalent to T step() calls without terminal observations: the env's
-        scalars, reward and done show the last step afterwards; its own obs planes show it too,
-        copied from planes[T-1] only when first needed (render(), the wrappers' observation(),
-        a masked reset), so modify the returned planes in place only after that or a later
-        step()/reset().  terminal_observation is not updated (it keeps the last step()'s)."""
+        scalars, reward and done show the last step afterwards, and so do its own obs planes
+        (planes[T-1] is copied into them on the same stream, right after the launch, so every obs
+        tuple reset()/step() returned is consistent).  terminal_observation is not updated (it
+        keeps the last step()'s)."""
         t = self._torch
         a = t.as_tensor(actions, device=self.device)
         if a.dim() != 2 or a.shape[1] != self.num_envs:
@@ -304,7 +324,7 @@ class BatchedWolvesAndBushesEnv:
                    "wab_rollout")
         if T > 0:  # the env's buffers show the last step, as after T step() calls
             self._sync_last_step(scal[:, T - 1], rew[T - 1], done[T - 1])
-            self._pending_planes = planes[T - 1]
+            self._obs["planes"].copy_(planes[T - 1])
         return planes, scal.permute(1, 0, 2), rew, done
 
     def _sync_last_step(self, scal, rew, done):
@@ -366,10 +386,9 @@ class BatchedWolvesAndBushesEnv:
             # render() of the env's own buffer then raise)
             self._sync_last_step(scal[:, T - 1], rew[T - 1], done[T - 1])
             if planes is not None:
-                self._pending_planes = planes[T - 1]
+                self._obs["planes"].copy_(planes[T - 1])
             else:
                 self._planes_valid = False
-                self._pending_planes = None
         return {"features": features, "scalars": scal.permute(1, 0, 2), "reward": rew, "done": done,
                 "returns": ret, "planes": planes}
 
@@ -402,13 +421,7 @@ class BatchedWolvesAndBushesEnv:
         del keep
         return img
 
-    def _materialize_planes(self):
-        if self._pending_planes is not None:
-            self._obs["planes"].copy_(self._pending_planes)
-            self._pending_planes = None
-
     def _require_planes(self):
-        self._materialize_planes()
         if not self._planes_valid:
             raise RuntimeError("the env's obs planes were not stored by the last call "
                                "(step_features/rollout_features with store_planes=False); pass obs= "

@@ -43,7 +43,7 @@ TYPES = ("Ostrich", "Wolf", "Bush")
 class BatchedWABEnvironment2:
     def __init__(self, world_width=32, world_height=32, game_options=None, num_ostriches=1,
                  num_wolves=8, num_bushes=16, num_worlds=4096, seed=0x5EED, device="cuda",
-                 world_id_base=0, autoreset=True):
+                 world_id_base=0, autoreset=True, spawn_positions=None):
         import torch
 
         self._torch = torch
@@ -67,8 +67,13 @@ class BatchedWABEnvironment2:
         self.R = lib.wab2_record_size(ctypes.addressof(self.cfg))
         _lib.check2(self.R if self.R < 0 else 0, "wab2_record_size")
         h = ctypes.c_void_p()
-        _lib.check2(lib.wab2_create(ctypes.addressof(self.cfg), self.num_worlds, self.seed,
-                                    self.world_id_base, dev.index, ctypes.byref(h)), "wab2_create")
+        # create_*(n, spawn_positions) (WAB_Environment2.py:61-110): [N, 2] for every world alike
+        # or [B, N, 2], entity-id order; a negative pair takes that entity's random position
+        pos = None if spawn_positions is None else self._positions(spawn_positions)
+        _lib.check2(lib.wab2_create_at(ctypes.addressof(self.cfg), self.num_worlds, self.seed,
+                                       self.world_id_base, dev.index,
+                                       None if pos is None else pos.ctypes.data, ctypes.byref(h)),
+                    "wab2_create_at")
         self._h = h
         B, N = self.num_worlds, self.N
         self.obs = torch.zeros((B, N, self.R), dtype=torch.uint8, device=dev)
@@ -104,17 +109,37 @@ class BatchedWABEnvironment2:
             a = a.to(t.int8)
         return a.to(self.device).contiguous()
 
+    def _positions(self, pos):
+        """Host int32 [B, N, 2] from [N, 2] (every world alike) or [B, N, 2] positions."""
+        if hasattr(pos, "cpu"):
+            pos = pos.cpu().numpy()
+        a = np.asarray(pos)
+        if a.dtype.kind not in "iu":
+            raise ValueError("positions must be integers")
+        if a.shape == (self.N, 2):
+            a = np.broadcast_to(a, (self.num_worlds, self.N, 2))
+        if a.shape != (self.num_worlds, self.N, 2):
+            raise ValueError("positions must have shape (%d, 2) or (%d, %d, 2)" % (self.N, self.num_worlds, self.N))
+        if a.size and (a.max() > 2**31 - 1 or a.min() < -2**31):
+            raise ValueError("positions must fit int32")
+        return np.ascontiguousarray(a, dtype=np.int32)
+
     # ------------------------------------------------------------------ the reference surface
-    def reset_environment(self, mask=None):
-        """WAB_Environment2.reset_environment (:113-118) of every world, or of the masked ones."""
+    def reset_environment(self, mask=None, positions=None):
+        """WAB_Environment2.reset_environment (:113-118) of every world, or of the masked ones.
+        positions ([N, 2] or [B, N, 2] ints, host or device) give each entity's
+        WAB_Environment2_Single.reset(new_x, new_y) (:36-41): a pair with a negative coordinate
+        draws the random position, as the reference does; this call then synchronises."""
         t = self._torch
         m = None
         if mask is not None:
             m = t.as_tensor(mask).to(device=self.device, dtype=t.uint8).contiguous()
             if tuple(m.shape) != (self.num_worlds,):
                 raise ValueError("mask must have shape (%d,)" % self.num_worlds)
-        _lib.check2(_lib.load().wab2_reset(self._h, None if m is None else m.data_ptr(), self._stream()),
-                    "wab2_reset")
+        pos = None if positions is None else self._positions(positions)
+        _lib.check2(_lib.load().wab2_reset_at(self._h, None if m is None else m.data_ptr(),
+                                              None if pos is None else pos.ctypes.data, self._stream()),
+                    "wab2_reset_at")
         self._keep = m
 
     def step(self, actions):
