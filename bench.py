@@ -172,6 +172,55 @@ def finite(x):
     return x
 
 
+class ClockSampler:
+    """The device's shader clock while a timed window runs, sampled every ~5 ms by a host thread
+    from sysfs (hwmon freq1_input, else the current level of pp_dpm_sclk): the DVFS evidence
+    beside each line (`sclk_mhz`: median, min, max, samples; None where sysfs has no clock)."""
+
+    def __init__(self, pci):
+        import glob
+
+        base = "/sys/bus/pci/devices/%s.0" % pci
+        self.hwmon = sorted(glob.glob(base + "/hwmon/hwmon*/freq1_input"))
+        self.dpm = base + "/pp_dpm_sclk"
+        self.last = None
+
+    def read(self):
+        try:
+            if self.hwmon:
+                return int(open(self.hwmon[0]).read()) / 1e6
+            for ln in open(self.dpm):
+                if ln.rstrip().endswith("*"):
+                    return float(ln.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+        except (OSError, ValueError, IndexError):
+            return None
+        return None
+
+    def __enter__(self):
+        import threading
+
+        self.samples, self.stop = [], threading.Event()
+
+        def loop():
+            while not self.stop.wait(0.005):
+                v = self.read()
+                if v is not None:
+                    self.samples.append(v)
+        self.th = threading.Thread(target=loop, daemon=True)
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+        v = sorted(self.samples)
+        self.last = None if not v else {"median": v[len(v) // 2], "min": v[0], "max": v[-1], "samples": len(v)}
+        return False
+
+
+CLOCK = None  # a ClockSampler of the bench's device (main), read by time_launches
+
+
 def time_launches(launch, n, dev, stream, mode="graph", min_seconds=MIN_TIMED_SECONDS, shards=1):
     """Average duration of one of `n` back-to-back launches (launch(i, hip_stream), or with
     shards > 1 launch(i, hip_stream, k) for every shard k, shard k's chain on its own stream
@@ -218,11 +267,14 @@ def time_launches(launch, n, dev, stream, mode="graph", min_seconds=MIN_TIMED_SE
     e1.record(stream)
     torch.cuda.synchronize(dev)
     reps = window_replays(e0.elapsed_time(e1) * 1e-3, min_seconds)
-    e0.record(stream)
-    for _ in range(reps):
-        once()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
+    import contextlib
+
+    with CLOCK if CLOCK is not None else contextlib.nullcontext():
+        e0.record(stream)
+        for _ in range(reps):
+            once()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
     return e0.elapsed_time(e1) / (reps * n), reps * n
 
 
@@ -290,7 +342,8 @@ def extra_configs(args, dev, B):
     def entry(us, alg, key, kernel, spl, n, api):
         return {"api": api, "us_per_step": round(us, 3), "env_steps_per_s": round(B / (us * 1e-6), 1),
                 "launches_timed": n, "steps_per_launch": spl,
-                "roofline": roofline_entry(alg, us, B, key, kernel, spl)}
+                "roofline": roofline_entry(alg, us, B, key, kernel, spl),
+                "sclk_mhz": CLOCK.last if CLOCK is not None else None}
 
     # the rollout entries as the main line runs them: the batch as S shards of Bs envs, each
     # shard's launches on its own stream (--stream-shards)
@@ -508,12 +561,14 @@ def run_torus(args, dev, rank, world):
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_wall = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(reps):
-        replay_once()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
+    with CLOCK:
+        ev0.record(stream)
+        for _ in range(reps):
+            replay_once()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t_wall
+    line_sclk = CLOCK.last
     stream_ms = ev0.elapsed_time(ev1)
     if world > 1:
         dist.barrier()
@@ -570,6 +625,7 @@ def run_torus(args, dev, rank, world):
                              "floor": {"min_launches": MIN_TIMED_LAUNCHES, "min_seconds": MIN_TIMED_SECONDS}},
             "warmup_effective": W,
             "devices": sorted({r["pci"] for r in per_rank}),
+            "sclk_mhz": line_sclk,
         }
         if world > 1:
             line["per_rank"] = per_rank
@@ -648,6 +704,26 @@ def cpu_baseline(opts, stride, seconds, threads, with_features=False):
             "sample": "oracle/wab_oracle.c %s, %d envs x %d steps (%.1f s) of the same workload, "
                       "OpenMP over envs" % (what, Bc, n, el) if threads > 1 else
                       "oracle/wab_oracle.c %s, %d envs x %d steps (%.1f s), 1 thread" % (what, Bc, n, el)}
+
+
+def config_cpu_baselines(line, threads, seconds):
+    """Each `configs` entry's own CPU baseline (the C oracle on this host's cores, a bounded
+    sample of that entry's workload, outside every timed region): C3 at 31x31 in 32-byte rows,
+    C5's step + featurizer, the torus world; the default per-step ring is the headline's own
+    workload (its `cpu_baseline`)."""
+    cfgs = line["configs"]
+    wopts, wstride = CONFIGS["wide31"][0], CONFIGS["wide31"][1]
+    if "wide31_rollout" in cfgs or "wide31_per_step_ring" in cfgs:
+        wb = cpu_baseline(wopts, wstride, seconds, threads)
+        for k in ("wide31_rollout", "wide31_per_step_ring"):
+            if k in cfgs:
+                cfgs[k]["cpu_baseline"] = wb
+    if "c5_rollout" in cfgs:
+        cfgs["c5_rollout"]["cpu_baseline"] = cpu_baseline(CONFIGS["c5"][0], CONFIGS["c5"][1], seconds, threads, True)
+    if "default_per_step_ring" in cfgs:
+        cfgs["default_per_step_ring"]["cpu_baseline"] = dict(line["cpu_baseline"], same_as="cpu_baseline")
+    if "torus_rollout" in cfgs:
+        cfgs["torus_rollout"]["cpu_baseline"] = torus_cpu_baseline(seconds, threads)
 
 
 def make_policy(F, n_actions, dev, seed=0):
@@ -794,20 +870,19 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from wab_gym_amd.shard import all_gather_objects, env_id_base, max_over_ranks, rank_info
+    from wab_gym_amd.shard import all_gather_objects, device_for_rank, env_id_base, max_over_ranks, rank_info
 
     rank, world, local = rank_info()
     if world != args.gpus:
         print("bench.py: --gpus %d but WORLD_SIZE=%d; the line reports WORLD_SIZE" % (args.gpus, world),
               file=sys.stderr)
     ndev = torch.cuda.device_count()
-    if world > ndev and not args.share_gpu and local >= ndev:
-        raise SystemExit("bench.py: rank %d has no GPU of its own (%d visible); pass --share-gpu"
-                         % (rank, ndev))
-    # ranks share a GPU when there are fewer GPUs than ranks (the 1-GPU rehearsal of N > 1)
-    local = local % max(1, ndev)
+    # LOCAL_RANK r -> GPU r; ranks share a GPU only when asked (--share-gpu: the 1-GPU rehearsal)
+    local = device_for_rank(local, ndev, args.share_gpu)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    global CLOCK
+    CLOCK = ClockSampler(pci_id(dev))
     if world > 1:
         dist.init_process_group("gloo")  # CPU only: barrier + timing MAX; no RCCL
 
@@ -1053,12 +1128,14 @@ def main():
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(reps):
-        replay_once()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
+    with CLOCK:  # (a host thread reading sysfs: nothing on the device's path)
+        ev0.record(stream)
+        for _ in range(reps):
+            replay_once()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
     wall_rank = time.perf_counter() - t0
+    line_sclk = CLOCK.last
     # each rank's time is its own launch stream's, from the HIP events around the window; the
     # MAX over ranks is taken afterwards (no barrier inside the window)
     stream_ms = ev0.elapsed_time(ev1)
@@ -1320,6 +1397,7 @@ def main():
             line["rollout"] = roll_line
         else:
             line["roofline"]["kernel_us_single_launch_median"] = round(single_ms * 1e3, 3)
+        line["sclk_mhz"] = line_sclk
         if world == 1 and args.config == "default" and rollout and not args.no_extra:
             # C3, C5, the per-step surfaces and the torus world beside the headline (their own
             # roofline each; the headline fields above are the default config's alone)
@@ -1329,6 +1407,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(opts, stride, args.cpu_seconds, cores["used"], c5)
             line["cpu_baseline"]["host"] = cores
             line["cpu_baseline_1t"] = cpu_baseline(opts, stride, args.cpu_seconds / 2, 1, c5)
+            if "configs" in line:
+                config_cpu_baselines(line, cores["used"], min(args.cpu_seconds, 5.0))
         print(json.dumps(finite(line), allow_nan=False), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -76,7 +76,6 @@ extern "C" {
 #define WAB2_MAX_ENTITIES 32  /* num_ostriches + num_wolves + num_bushes */
 #define WAB2_MAX_OSTRICHES 8
 #define WAB2_MAX_SIDE 127     /* width, height (deltas are int8) */
-#define WAB2_MAX_POSITION (1 << 20) /* explicit reset positions (wab2_reset_at) */
 #define WAB2_MAX_RADIUS (1 << 20) /* view radii (a radius past the world's diagonal already sees all of it) */
 
 #define WAB2_OK 0
@@ -153,9 +152,10 @@ int wab2_reset(wab2_handle* h, const uint8_t* mask, void* stream);
  * WAB_Environment2_Single.reset(new_x, new_y) (WAB_Environment2_Single.py:36-41), then
  * World.reset_world.  positions: HOST int32 [B][N][2] or NULL (= wab2_reset); a pair with a
  * negative coordinate draws the random position (randint(0, W), randint(0, H), as the reference
- * does for new_x < 0 or new_y < 0), others lie in [0, WAB2_MAX_POSITION]^2 (the entity's own,
- * unbounded coordinates; its frame X/Y stay stale until it acts, as after any reset).  Entries
- * of unmasked worlds are ignored.  Synchronises `stream` when positions != NULL. */
+ * does for new_x < 0 or new_y < 0), others lie in [0, W] x [0, H], the range of those random
+ * draws (the reference takes any integers; its frame X/Y stay stale until the entity acts, as
+ * after any reset).  Entries of unmasked worlds are ignored.  Synchronises `stream` when
+ * positions != NULL. */
 int wab2_reset_at(wab2_handle* h, const uint8_t* mask, const int32_t* positions, void* stream);
 
 /* One turn of every world.  actions [B][N] int8 (any value: those outside an entity's act

@@ -73,7 +73,7 @@ SETS = {
     "torus_continue": (16, 16, (1, 3, 5), {}, list(range(300, 304)), 140, "continue"),
     # caller-chosen positions: create_*(n, spawn_positions) and each entity's
     # reset(new_x, new_y) (WAB_Environment2.py:61-110, WAB_Environment2_Single.py:36-41) at turns
-    # 0, 30 and 61, a quarter of them negative (the random position), some past the world's edge;
+    # 0, 30 and 61, a quarter of them negative (the random position), some on the far edge;
     # the World_tests.py world size
     "torus_placed": (20, 20, (2, 3, 4), {"lookout_view_radius": 10, "gatherer_view_radius": 8,
                                          "wolf_view_radius": 6, "max_turns": 40},
@@ -86,7 +86,7 @@ PLACED_RESETS = {"torus_placed": (0, 30, 61)}
 
 def placed_positions(e, W, H, N, k):
     """The placed set's positions of world index e: k = -1 create (tiles of the world), k >= 0
-    the k-th explicit reset ((-1, -1) = random, x or y = W/H, beyond the edge, or a tile)."""
+    the k-th explicit reset ((-1, -1) = random, x = W or y = H, or a tile)."""
     rng = np.random.RandomState(7000 + 97 * e + k)
     if k < 0:
         return np.stack([rng.randint(W, size=N), rng.randint(H, size=N)], -1).astype(np.int32)
@@ -95,8 +95,8 @@ def placed_positions(e, W, H, N, k):
         u = rng.random_sample()
         if u < 0.25:
             out[i] = (-1, -1) if rng.random_sample() < 0.5 else (-1 - rng.randint(3), rng.randint(H))
-        elif u < 0.4:
-            out[i] = (rng.choice([W, 2 * W + 3, 100]), rng.choice([H, rng.randint(H), 57]))
+        elif u < 0.4:  # on the far edges, x = W or y = H (as randint(0, W) draws them too)
+            out[i] = (W, rng.randint(H + 1)) if rng.random_sample() < 0.5 else (rng.randint(W + 1), H)
         else:
             out[i] = (rng.randint(W + 1), rng.randint(H + 1))
     return out

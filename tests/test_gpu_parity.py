@@ -1139,7 +1139,7 @@ def test_env_step_into_obs_ring_fresh_placement():
             assert np.array_equal(ring[t % 3]["planes"].cpu().numpy(), op), t
             assert np.array_equal(obs[3].cpu().numpy(), of), t
             assert np.array_equal(rew.cpu().numpy(), orew), t
-            kept.append(op)
+            kept.append(op.copy())  # (the oracle returns its own buffer)
             if t >= 2:  # the slot written two steps ago still holds its step
                 assert np.array_equal(ring[(t - 2) % 3]["planes"].cpu().numpy(), kept[t - 2]), t
         with pytest.raises(RuntimeError):

@@ -374,7 +374,7 @@ def test_torus_world_tests_wrap_kat_on_gpu():
 
 def test_torus_explicit_positions_lockstep_vs_oracle():
     """wab2_create_at / wab2_reset_at (explicit positions, a quarter of them negative = the
-    keyed random draw, reset positions up to 3 sides past the edge) at B = 4096, 1/8/16, against
+    keyed random draw, reset positions on the far edges x = W, y = H too) at B = 4096, 1/8/16, against
     the oracle given the same positions: full and masked resets, 60 turns, every record."""
     import torch
 
@@ -391,7 +391,7 @@ def test_torus_explicit_positions_lockstep_vs_oracle():
     hi = np.array([6] + [5] * 8 + [1] * 16)
     for t in range(60):
         if t % 20 == 0:
-            pos = np.stack([rng.randint(3 * W + 1, size=(B, N)), rng.randint(H + 1, size=(B, N))], -1)
+            pos = np.stack([rng.randint(W + 1, size=(B, N)), rng.randint(H + 1, size=(B, N))], -1)
             pos[rng.random_sample((B, N)) < 0.25] = (-1, 5)
             mask = None if t == 0 else (rng.random_sample(B) < 0.5).astype(np.uint8)
             env.reset_environment(mask=mask, positions=pos.astype(np.int32))
@@ -409,4 +409,4 @@ def test_torus_explicit_positions_lockstep_vs_oracle():
         BatchedWABEnvironment2(W, H, None, 1, 8, 16, num_worlds=2, device="cuda:0",
                                spawn_positions=np.full((N, 2), W, np.int32))  # x = W is not a tile
     with pytest.raises(Exception):
-        env.reset_environment(positions=np.full((N, 2), (1 << 20) + 1, np.int64))
+        env.reset_environment(positions=np.full((N, 2), W + 1, np.int64))  # past randint(0, W)

@@ -62,3 +62,19 @@ def test_bench_refuses_more_ranks_than_gpus():
     assert r.returncode != 0
     assert "--share-gpu" in r.stderr
     assert not r.stdout.strip()
+
+
+def test_ranks_bind_distinct_devices():
+    """One process per GPU: on an 8-GPU node ranks 0..7 bind devices 0..7, each its own; with
+    fewer GPUs than ranks a rank without a GPU is refused unless the run shares them."""
+    import pytest
+
+    from wab_gym_amd.shard import device_for_rank
+
+    assert [device_for_rank(r, 8) for r in range(8)] == list(range(8))
+    assert [device_for_rank(r, 4) for r in range(4)] == [0, 1, 2, 3]
+    assert [device_for_rank(r, 1, share_gpu=True) for r in range(2)] == [0, 0]
+    with pytest.raises(SystemExit):
+        device_for_rank(1, 1)
+    with pytest.raises(SystemExit):
+        device_for_rank(0, 0)

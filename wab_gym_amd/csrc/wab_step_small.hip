@@ -599,47 +599,6 @@ __device__ __forceinline__ void early_view_zeros(const Params& p, uint32_t e0, u
   view_zero_lines(p.features + (size_t)blockIdx.x * 64u * F, F, e0, n_rows, lane, 64);
 }
 
-// --------------------------------------------------------------------------- early ostrich plane
-// The ostrich plane of every observation (:393-444) is the same: the ostrich's own cell, set
-// (mask_grid never blinds it), in an otherwise empty grid, a new episode's included.  Per-step
-// launches of the default geometry (G = 11) store the 16-byte units that lie wholly inside an
-// env's ostrich plane (424 of a group's 1452 units) right after B_init, while the HBM is
-// otherwise idle but for the state reads, and the final store (store_obs) skips them: a third
-// of the obs bytes leave the end phase.  Env e's plane is bytes [e OB + 2 WH, (e + 1) OB) of the
-// group's chunk; its whole units are u in [ceil((e OB + 2 WH) / 16), floor((e + 1) OB / 16)).
-// (-DWAB_EARLY_OSTRICH=0: the A/B baseline, every unit stored at the end; tools/build_variants.sh)
-#ifndef WAB_EARLY_OSTRICH
-#define WAB_EARLY_OSTRICH 1
-#endif
-template <int G>
-__device__ __forceinline__ bool ostrich_only_unit(uint32_t u) {
-  static_assert(G == 11, "the early ostrich plane is specialised to the default geometry");
-  constexpr uint32_t OB = 363, WH = 121;
-  const uint32_t off = (16u * u) % OB;
-  return off >= 2u * WH && off + 16u <= OB;
-}
-template <int G>
-__device__ __forceinline__ void early_ostrich_units(const Params& p, int lane) {
-  static_assert(G == 11, "the early ostrich plane is specialised to the default geometry");
-  constexpr uint32_t OB = 363, WH = 121, CB = 2u * WH + 5u * 11u + 5u;  // the centre cell's byte
-  const int64_t g0 = (int64_t)blockIdx.x * 64;
-  if (g0 + lane >= p.B) return;
-  const uint32_t e0 = (uint32_t)lane * OB;
-  const uint32_t u0 = (e0 + 2u * WH + 15u) >> 4, u1 = (e0 + OB) >> 4;
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4* out = reinterpret_cast<u32x4*>(p.planes + (size_t)g0 * OB);
-#pragma unroll
-  for (uint32_t k = 0; k < 7u; ++k) {  // 6 or 7 units per env
-    const uint32_t u = u0 + k;
-    if (u >= u1) break;
-    const uint32_t c = e0 + CB - 16u * u;  // the centre byte's offset in the unit (or out of it)
-    u32x4 q = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (uint32_t w = 0; w < 4u; ++w) q[w] = (c >> 2) == w ? 1u << (8u * (c & 3u)) : 0u;
-    out[u] = q;
-  }
-}
-
 // --------------------------------------------------------------------------- fused returns
 // wab_rollout_features: each step W0 keeps its env's reward as a code in LDS (ate, the outcome,
 // done), and after the last step runs finish_episode's scan over the launch's steps
@@ -1313,9 +1272,6 @@ __device__ __forceinline__ unsigned long long ring_wave(const Params& p, const S
   }
   const Head h = head_decode(p, g, g < p.B, hr);
   if (!ROLL || t == 0) lds_barrier();  // B_init
-  if constexpr (G == 11 && !ROLL && WAB_EARLY_OSTRICH) {
-    if (p.planes) early_ostrich_units<G>(p, lane);
-  }
   if (p.features) {
     if (!ROLL || t == 0)
       feat_tables_build(feat_tables_at(lds + L.ftab, p.W / 2 + p.H / 2 + 1), p.W, p.H, p.W / 2 + p.H / 2 + 1, lane, 64);
@@ -1408,7 +1364,7 @@ __device__ __forceinline__ void store_units_of(const Params& p, uint32_t* stream
   }
 }
 
-template <int G = 0, bool CLEAR = false>
+template <bool CLEAR = false>
 __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int tid) {
   const int64_t g0 = (int64_t)blockIdx.x * 64;
   const uint32_t OB = (uint32_t)p.OB;
@@ -1437,9 +1393,6 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
   for (int k = 0; k < 6; ++k) {
     const uint32_t u = (uint32_t)tid + 256u * (uint32_t)k;
     if (u >= full) break;
-    if constexpr (G == 11 && WAB_EARLY_OSTRICH) {
-      if (ostrich_only_unit<G>(u)) continue;  // stored after B_init (early_ostrich_units)
-    }
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     u32x4 q;
 #pragma unroll
@@ -1616,7 +1569,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
     const Params p = wave_params<G, FEAT>(p0);
     const SmallLayout L = small_layout(p);
     (void)jm;
-    if (!FEAT || p.planes) store_obs<G>(p, lds + L.stream, threadIdx.x);
+    if (!FEAT || p.planes) store_obs(p, lds + L.stream, threadIdx.x);
     if constexpr (FEAT) step_features(p, L, lds, wave, lane);
   } else {
     // wab_rollout: n_steps steps of this group, one after the other (the envs of a workgroup

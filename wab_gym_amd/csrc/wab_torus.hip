@@ -417,6 +417,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   }
   lds_barrier();
 
+  // (tuning A/B, tools/build_variants.sh -DWAB2_STAGGER=k: the odd dispatch rounds' workgroups
+  // start k x ~3.5 us late, so that a CU's groups are not all in phase A / C at once)
+#ifndef WAB2_STAGGER
+#define WAB2_STAGGER 0
+#endif
+  if (WAB2_STAGGER && ((blockIdx.x >> 8) & 1u))
+    for (int k = 0; k < WAB2_STAGGER; ++k) __builtin_amdgcn_s_sleep(127);
   int64_t resets = 0;
   for (int t = 0; t < T; ++t) {
     WAB2_STAMP(0);
@@ -1387,7 +1394,9 @@ int wab2_reset_at(wab2_handle* h, const uint8_t* mask, const int32_t* positions,
     return fail(WAB2_E_INVALID, "wab2_reset: a masked reset only between turns (entity " +
                                     std::to_string(h->next_entity) + " acts next)");
   const TParams& hp = h->p;
-  const std::string pv = check_positions(positions, hp.B, hp.N, WAB2_MAX_POSITION, WAB2_MAX_POSITION, "wab2_reset_at");
+  // the range of the random reset draws, randint(0, W) x randint(0, H) (a bush keeps its own x, y
+  // in a byte each and its frame X = x mod W is one subtraction)
+  const std::string pv = check_positions(positions, hp.B, hp.N, hp.W, hp.H, "wab2_reset_at");
   if (!pv.empty()) return fail(WAB2_E_INVALID, pv);
   h->next_entity = 0;  // reset_environment: num_entities_acted_this_turn = 0 (WAB_Environment2.py:117)
   DeviceGuard2 dg(h->device);

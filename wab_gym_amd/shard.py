@@ -110,3 +110,14 @@ def all_gather_objects(obj):
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, obj)
     return out
+
+
+def device_for_rank(local_rank, n_devices, share_gpu=False):
+    """The GPU index rank `local_rank` binds (one process per GPU: LOCAL_RANK r -> device r).  With
+    fewer visible GPUs than ranks it raises unless share_gpu (the 1-GPU rehearsal of N > 1, ranks
+    then share device local_rank % n_devices)."""
+    if n_devices < 1:
+        raise SystemExit("no GPU visible")
+    if local_rank >= n_devices and not share_gpu:
+        raise SystemExit("rank %d has no GPU of its own (%d visible); pass --share-gpu" % (local_rank, n_devices))
+    return local_rank % n_devices
