@@ -1397,7 +1397,11 @@ __device__ __forceinline__ void store_obs(const Params& p, uint32_t* stream, int
     u32x4 q;
 #pragma unroll
     for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
+#ifndef WAB_STEP_OBS_NT  // (tuning A/B: 0 = plain stores)
+#define WAB_STEP_OBS_NT 1
+#endif
+    if (WAB_STEP_OBS_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);  // streamed: no L2 allocation
+    else reinterpret_cast<u32x4*>(out)[u] = q;
   }
   for (uint32_t b = (full << 4) + tid; b < limit; b += 256)  // a partial last group
     out[b] = (uint8_t)((stream[b >> 5] >> (b & 31)) & 1u);

@@ -357,19 +357,6 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
   return pair & (0u - ok);
 }
 
-// The record stage: record r of a wave's 32 at r R bytes, its 16-byte chunks rotated by one for
-// r in [4, 8) mod 8 (chunk c at ((c + rot) mod CR) 16): the 32 lanes that write one dword of
-// their records then hit 8 banks at R = 96 instead of 4 (4-way conflicts instead of 8-way), the
-// 8-lane groups of a 16-byte write none; the copy-out reads whole chunks, un-rotated by address.
-#ifndef WAB2_SWZ
-#define WAB2_SWZ 1
-#endif
-__device__ __forceinline__ uint8_t* stage_at(uint8_t* stage, int r, int off, int R, int CR) {
-  int c = (off >> 4) + (WAB2_SWZ ? (r >> 2) & 1 : 0);
-  c = c >= CR ? c - CR : c;
-  return stage + r * R + c * 16 + (off & 15);
-}
-
 // NKK = ceil(N / 4): dword-pair groups of the delta array.  CNO, CNW, CNB > 0: an instance for
 // whole turns (windows [0, N)) of those entity counts, whose table layout, record size, loop
 // bounds and divisions are compile-time constants (the benched 1 / 8 / 16 world); 0: the counts
@@ -653,16 +640,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               const int q0 = rnd * 64 + 32 * half;
               if (q0 >= nitems) break;  // (uniform)
               if (hf == half) {
-                const int rr = lane & 31;
-                *reinterpret_cast<uint4*>(stage_at(stage, rr, 0, R, CR)) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8);
-                *reinterpret_cast<uint2*>(stage_at(stage, rr, 16, R, CR)) = make_uint2(vis, (uint32_t)T_BUSH << 16);
+                uint8_t* rec = stage + (lane & 31) * R;
+                *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8);
+                *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, (uint32_t)T_BUSH << 16);
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
                 for (int k = 0; k < ((WAB2_ABLATE & 4) ? 0 : ndw); ++k) {
                   uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
                   if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
                   const uint32_t b4 = (uint32_t)(v64 >> (NM + 4 * k - sh + 8)) & 0xFu;
-                  *reinterpret_cast<uint32_t*>(stage_at(stage, rr, 4 * (d0 + k), R, CR)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                  *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
                 }
               }
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -676,7 +663,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
                 const int qq = q0 + r;
                 const int ww = (int)(((uint32_t)qq * magic_b) >> 20);
                 const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-                const u32x4 val = *reinterpret_cast<const u32x4*>(stage_at(stage, r, 16 * (c - r * CR), R, CR));
+                const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
                 __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
               }
               __builtin_amdgcn_wave_barrier();
@@ -788,18 +775,20 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             food = s.food[i * kWorlds + w];
           }
           const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
-          const int rr = lane & 31;
+          uint8_t* rec = stage + (lane & 31) * R;
           if (hf == 0) {
             const uint64_t fb = (uint64_t)__double_as_longlong(food);
-            *reinterpret_cast<uint4*>(stage_at(stage, rr, 0, R, CR)) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
-            *reinterpret_cast<uint2*>(stage_at(stage, rr, 16, R, CR)) = make_uint2(vis, flags | ((uint32_t)type << 16));
+            *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
+            *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
           } else if (!bush) {
-            for (int z = 24 + 4 * nd; z < R; z += 4) *reinterpret_cast<uint32_t*>(stage_at(stage, rr, z, R, CR)) = 0u;
+            // (only the pad past the bush-food bytes: the deltas and those bytes are written below
+            // in full, and nothing writes the pad non-zero; the stage is zeroed each turn)
+            for (int z = (bb + 2 * nbp + 3) & ~3; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
           }
           if (!bush) {  // (a bush's deltas are zero: the stage's, since the turn's first round)
 #pragma unroll
             for (int kk = 0; kk < NKK; ++kk)
-              if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(stage_at(stage, rr, 24 + 4 * (2 * kk + hf), R, CR)) = d[kk];
+              if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
           }
           // Additional_Data [food] of the visible bushes as the observer sees them: after the
           // eats of the ostriches that acted before it in this launch (bf1 for every observer
@@ -816,7 +805,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
               if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
               const uint32_t b4 = (uint32_t)(v64 >> (NM + b + 8)) & 0xFu;
-              *reinterpret_cast<uint32_t*>(stage_at(stage, rr, 4 * (d0 + k), R, CR)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+              *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
             }
           }
           for (int m = hf; m < ((bush || (WAB2_ABLATE & 4)) ? 0 : nbp); m += 2) {
@@ -833,7 +822,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             }
             const uint32_t vb = vis >> (NM + b);
             f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
-            *reinterpret_cast<uint16_t*>(stage_at(stage, rr, bb + b, R, CR)) = (uint16_t)f;
+            *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -849,7 +838,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const int qq = q0 + r;
             const int ww = (int)(((uint32_t)qq * magic) >> 20);
             const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-            const u32x4 val = *reinterpret_cast<const u32x4*>(stage_at(stage, r, 16 * (c - r * CR), R, CR));
+            const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
             __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
           }
           __builtin_amdgcn_wave_barrier();
@@ -895,16 +884,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               const int q0 = rnd * 64 + 32 * half;
               if (q0 >= nitems) break;  // (uniform)
               if (hf == half) {
-                const int rr = lane & 31;
-                *reinterpret_cast<uint4*>(stage_at(stage, rr, 0, R, CR)) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8);
-                *reinterpret_cast<uint2*>(stage_at(stage, rr, 16, R, CR)) = make_uint2(vis, (uint32_t)T_BUSH << 16);
+                uint8_t* rec = stage + (lane & 31) * R;
+                *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8);
+                *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, (uint32_t)T_BUSH << 16);
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
                 for (int k = 0; k < ((WAB2_ABLATE & 4) ? 0 : ndw); ++k) {
                   uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
                   if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
                   const uint32_t b4 = (uint32_t)(v64 >> (NM + 4 * k - sh + 8)) & 0xFu;
-                  *reinterpret_cast<uint32_t*>(stage_at(stage, rr, 4 * (d0 + k), R, CR)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                  *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
                 }
               }
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -918,7 +907,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
                 const int qq = q0 + r;
                 const int ww = (int)(((uint32_t)qq * magic_b) >> 20);
                 const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-                const u32x4 val = *reinterpret_cast<const u32x4*>(stage_at(stage, r, 16 * (c - r * CR), R, CR));
+                const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
                 __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
               }
               __builtin_amdgcn_wave_barrier();
