@@ -1044,7 +1044,12 @@ __device__ __forceinline__ unsigned long long wolves_wave(const Params& p, const
   // the first 8 slots load with the header, whatever the wolf count: a group of 64 envs
   // nearly always has a lane with more than 4 wolves, and loading the rest after the count
   // arrives costs a second memory round trip on the path to B1
-  constexpr int kSpecSlots = SLOTS < 8 ? SLOTS : 8;
+  // wolf slots read with the header, speculatively (the rest after B_init, for envs with more
+  // wolves); -DWAB_SPEC_WOLVES=k: the tuning A/B of that count
+#ifndef WAB_SPEC_WOLVES
+#define WAB_SPEC_WOLVES 8
+#endif
+  constexpr int kSpecSlots = SLOTS < WAB_SPEC_WOLVES ? SLOTS : WAB_SPEC_WOLVES;
   uint32_t wr[SLOTS];
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) wr[k] = 0u;
