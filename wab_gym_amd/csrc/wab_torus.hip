@@ -352,9 +352,53 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
   const s16x2 nl = sign_mask2(P - v.lo);  // -1: P < lo (no wrap down)
   const s16x2 nr = sign_mask2(v.hi - P);  // -1: P > hi (no wrap up)
   const s16x2 d = P - v.e - (v.wh & ~nl) + (v.wh & ~nr);
-  ok = (uint32_t)(__builtin_amdgcn_sdot2(d, d, 0, false) <= v.r2);
+  // dx^2 + dy^2 as one v_dot2_i32_i16 with an inline-zero accumulator (the builtin becomes a
+  // v_mov of the zero and a v_dot2c)
+  int dd;
+  asm("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(dd) : "v"(__builtin_bit_cast(uint32_t, d)));
+  ok = (uint32_t)(dd <= v.r2);
   const uint32_t pair = __builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, d), 0x0c0c0200u);
   return pair & (0u - ok);
+}
+
+// A round's staged records out to HBM: chunk c (16 bytes) of stage slot r = c / CR is byte
+// 16 (c - r CR) of record qq = q0 + r of the round, world ww = qq / nc, at its place in the
+// [B][no][R] records; consecutive lanes on consecutive chunks.  Every LDS read of the lane is
+// issued before its first store (a loop waited for each read in turn); KMAX >= chunks / 64 (0:
+// the loop, for the generic instances, whose registers are at the ceiling).
+#ifndef WAB2_COPY_HOIST  // (tuning A/B: 0 = one chunk at a time, each read waited for before its store)
+#define WAB2_COPY_HOIST 1
+#endif
+template <int KMAX>
+__device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, int chunks, int lane, int q0, int w0r,
+                                         int no, int nc, int R, int CR, uint32_t magic_cr, uint32_t magic) {
+  if (!WAB2_COPY_HOIST || KMAX == 0) {  // (KMAX 0: the generic instances, at their VGPR ceiling)
+    for (int c = lane; c < chunks; c += 64) {
+      const int r = (int)(((uint32_t)c * magic_cr) >> 16);
+      const int qq = q0 + r;
+      const int ww = (int)(((uint32_t)qq * magic) >> 20);
+      const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(stage + 16 * c), reinterpret_cast<u32x4*>(rbase + off));
+    }
+    return;
+  }
+  constexpr int K = KMAX > 0 ? KMAX : 1;
+  u32x4 val[K];
+  uint32_t off[K];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int c = lane + 64 * k;
+    if (c < chunks) {
+      const int r = (int)(((uint32_t)c * magic_cr) >> 16);  // stage slot: c / CR
+      const int qq = q0 + r;
+      const int ww = (int)(((uint32_t)qq * magic) >> 20);
+      off[k] = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
+      val[k] = *reinterpret_cast<const u32x4*>(stage + 16 * c);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (lane + 64 * k < chunks) __builtin_nontemporal_store(val[k], reinterpret_cast<u32x4*>(rbase + off[k]));
 }
 
 // NKK = ceil(N / 4): dword-pair groups of the delta array.  CNO, CNW, CNB > 0: an instance for
@@ -591,6 +635,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       const int bb = 24 + 2 * N;          // first bush-food byte
       const int nbp = (NB + 1) >> 1;      // bush-food byte pairs
       const int CR = R >> 4;              // 16-byte chunks per record
+      // chunks per lane of a 32-record copy-out: 32 CR / 64 (R <= 128 bytes: at most 4)
+      constexpr int kCopyMax = kFixed ? (32 * ((24 + 2 * kN + CNB + 15) / 16) + 63) / 64 : 0;
       const uint32_t exist = N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u;
       // the stage starts zero: the bush rounds (first) then write only their headers and bush
       // bytes (their deltas are zero); the mover rounds write every byte
@@ -614,6 +660,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const int qc = on ? q : nitems - 1;
             const int w = (int)(((uint32_t)qc * magic_b) >> 20);
             const int i = c0 + qc - w * nc;
+            // (the fixed instance: a bush observer; every mover has acted before it)
+            if (kFixed) __builtin_assume(i >= NM && i < N);
             const uint32_t* posw = s.pos + w * Np;
             const uint32_t tgt = posw[i] & 0xFFFFu;  // (its frame X/Y before its act)
             // every wolf acts before a bush: the Visible ostriches of Lds::alv[NM]
@@ -658,14 +706,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               const int chunks = min(32, nitems - q0) * CR;
               const int w0r = (int)(((uint32_t)q0 * magic_b) >> 20);
               uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;
-              for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-                const int r = (int)(((uint32_t)c * magic_cr) >> 16);
-                const int qq = q0 + r;
-                const int ww = (int)(((uint32_t)qq * magic_b) >> 20);
-                const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-                const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
-                __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
-              }
+              copy_out<kCopyMax>(stage, rbase, (WAB2_ABLATE & 2) ? 0 : chunks, lane, q0, w0r, no, nc, R, CR, magic_cr, magic_b);
               __builtin_amdgcn_wave_barrier();
             }
           }
@@ -687,6 +728,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
           const int w = (int)(((uint32_t)qc * magic) >> 20);
           const int i = c0 + qc - w * nc;
+          // (the fixed instance: a mover observer; every entity from NM on is then seen at its
+          // position before the launch, with no per-entity select)
+          if (kFixed) __builtin_assume(i >= 0 && i < NM);
           const int type = bush ? T_BUSH : i < NO ? T_OSTRICH : T_WOLF;
           const uint32_t* posw = s.pos + w * Np;
           const uint32_t pi = posw[i];
@@ -833,14 +877,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int chunks = min(32, nitems - q0) * CR;
           const int w0r = (int)(((uint32_t)q0 * magic) >> 20);  // the round's first world
           uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;  // its first record
-          for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-            const int r = (int)(((uint32_t)c * magic_cr) >> 16);  // stage slot: c / CR
-            const int qq = q0 + r;
-            const int ww = (int)(((uint32_t)qq * magic) >> 20);
-            const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-            const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
-            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
-          }
+          copy_out<kCopyMax>(stage, rbase, (WAB2_ABLATE & 2) ? 0 : chunks, lane, q0, w0r, no, nc, R, CR, magic_cr, magic);
           __builtin_amdgcn_wave_barrier();
         }
       }
@@ -858,6 +895,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const int qc = on ? q : nitems - 1;
             const int w = (int)(((uint32_t)qc * magic_b) >> 20);
             const int i = c0 + qc - w * nc;
+            // (the fixed instance: a bush observer; every mover has acted before it)
+            if (kFixed) __builtin_assume(i >= NM && i < N);
             const uint32_t* posw = s.pos + w * Np;
             const uint32_t tgt = posw[i] & 0xFFFFu;  // (its frame X/Y before its act)
             // every wolf acts before a bush: the Visible ostriches of Lds::alv[NM]
@@ -902,14 +941,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               const int chunks = min(32, nitems - q0) * CR;
               const int w0r = (int)(((uint32_t)q0 * magic_b) >> 20);
               uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;
-              for (int c = lane; c < ((WAB2_ABLATE & 2) ? 0 : chunks); c += 64) {
-                const int r = (int)(((uint32_t)c * magic_cr) >> 16);
-                const int qq = q0 + r;
-                const int ww = (int)(((uint32_t)qq * magic_b) >> 20);
-                const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-                const u32x4 val = *reinterpret_cast<const u32x4*>(stage + 16 * c);
-                __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rbase + off));
-              }
+              copy_out<kCopyMax>(stage, rbase, (WAB2_ABLATE & 2) ? 0 : chunks, lane, q0, w0r, no, nc, R, CR, magic_cr, magic_b);
               __builtin_amdgcn_wave_barrier();
             }
           }
