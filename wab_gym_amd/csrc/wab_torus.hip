@@ -684,6 +684,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
             const uint64_t fb = (uint64_t)__double_as_longlong((double)row[i - NM]);
             const uint64_t v64 = (uint64_t)vis << 8;  // (bit NM + b + 8: bush b, b >= -8)
+            // the fixed instance: the row's dwords read once, before the halves' stage writes
+            // (which the compiler would otherwise order each row read behind)
+            constexpr int kRowW = kFixed ? (((24 + 2 * kN) & 3) + CNB + 3) / 4 : 1;
+            uint32_t rdw[kRowW];
+#pragma unroll
+            for (int k = 0; k < kRowW; ++k) rdw[k] = kFixed ? *reinterpret_cast<const uint32_t*>(row + 4 * k) : 0u;
             for (int half = 0; half < 2; ++half) {
               const int q0 = rnd * 64 + 32 * half;
               if (q0 >= nitems) break;  // (uniform)
@@ -693,6 +699,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
                 *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, (uint32_t)T_BUSH << 16);
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
+                if (kFixed) {
+#pragma unroll
+                  for (int k = 0; k < kRowW; ++k) {
+                    if (WAB2_ABLATE & 4) break;
+                    uint32_t x = rdw[k];
+                    if (sh) x = (x << (8 * sh)) | (k > 0 ? rdw[k > 0 ? k - 1 : 0] >> (32 - 8 * sh) : 0u);
+                    const uint32_t b4 = (uint32_t)(v64 >> (NM + 4 * k - sh + 8)) & 0xFu;
+                    *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                  }
+                } else
                 for (int k = 0; k < ((WAB2_ABLATE & 4) ? 0 : ndw); ++k) {
                   uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
                   if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
@@ -919,6 +935,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             const uint32_t bxy = s.bxy[(i - NM) * kWorlds + w];
             const uint64_t fb = (uint64_t)__double_as_longlong((double)row[i - NM]);
             const uint64_t v64 = (uint64_t)vis << 8;  // (bit NM + b + 8: bush b, b >= -8)
+            // the fixed instance: the row's dwords read once, before the halves' stage writes
+            // (which the compiler would otherwise order each row read behind)
+            constexpr int kRowW = kFixed ? (((24 + 2 * kN) & 3) + CNB + 3) / 4 : 1;
+            uint32_t rdw[kRowW];
+#pragma unroll
+            for (int k = 0; k < kRowW; ++k) rdw[k] = kFixed ? *reinterpret_cast<const uint32_t*>(row + 4 * k) : 0u;
             for (int half = 0; half < 2; ++half) {
               const int q0 = rnd * 64 + 32 * half;
               if (q0 >= nitems) break;  // (uniform)
@@ -928,6 +950,16 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
                 *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, (uint32_t)T_BUSH << 16);
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
+                if (kFixed) {
+#pragma unroll
+                  for (int k = 0; k < kRowW; ++k) {
+                    if (WAB2_ABLATE & 4) break;
+                    uint32_t x = rdw[k];
+                    if (sh) x = (x << (8 * sh)) | (k > 0 ? rdw[k > 0 ? k - 1 : 0] >> (32 - 8 * sh) : 0u);
+                    const uint32_t b4 = (uint32_t)(v64 >> (NM + 4 * k - sh + 8)) & 0xFu;
+                    *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                  }
+                } else
                 for (int k = 0; k < ((WAB2_ABLATE & 4) ? 0 : ndw); ++k) {
                   uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
                   if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
