@@ -256,6 +256,9 @@ __device__ __forceinline__ TParams kparams(const TParams& p0) {
 #endif
 }
 
+#ifndef WAB2_ACT_DRAIN  // (tuning A/B: 1 = drain the action loads; measured slower, below)
+#define WAB2_ACT_DRAIN 0
+#endif
 // actions of turn t for the workgroup's worlds into act (raw [64][N] bytes), by one wave:
 // dword loads, all issued before the first is used, when the slice is 4-byte aligned and the
 // workgroup is full (the wave's stores of the previous turn, which the same vmcnt counts, are
@@ -275,6 +278,12 @@ __device__ __forceinline__ void fetch_actions_wave(const TParams& p, int t, int6
 #pragma unroll
     for (int k = 0; k < kMax; ++k)
       if (lane + 64 * k < nd) d32[lane + 64 * k] = v[k];
+    // (the compiler's wait tracking carries these loads as pending into phase B, as it cannot
+    // tell that the lanes whose stores were skipped loaded nothing, and puts a vmcnt(0) - a
+    // wait for all of the wave's record stores - at the head of every bush round of every
+    // wave.  Retiring them here removes those waits, and measured slower: 47.57 -> 47.63 us
+    // per turn; the waits bound each wave's stores in flight to about one round)
+    if (WAB2_ACT_DRAIN) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
   } else {
     for (int q = lane; q < nbytes; q += 64)
       act[q] = q < nvalid * p.N ? (uint8_t)src[q] : (uint8_t)0;
@@ -369,6 +378,18 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
 #ifndef WAB2_COPY_HOIST  // (tuning A/B: 0 = one chunk at a time, each read waited for before its store)
 #define WAB2_COPY_HOIST 1
 #endif
+#ifndef WAB2_COPY_UNCOND  // (tuning A/B: 0 = each hoisted read under its chunk's bound)
+#define WAB2_COPY_UNCOND 1
+#endif
+#ifndef WAB2_DELTA_B64  // (tuning A/B: 0 = a mover's delta dwords one by one, vis by an LDS permute)
+#define WAB2_DELTA_B64 1
+#endif
+#ifndef WAB2_BUSH_WIDE  // (tuning A/B: 0 = a bush record's food dwords one by one)
+#define WAB2_BUSH_WIDE 1
+#endif
+#ifndef WAB2_MOVER_ROW128  // (tuning A/B: 0 = a mover round's bush-food pairs read one by one)
+#define WAB2_MOVER_ROW128 1
+#endif
 template <int KMAX>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, int chunks, int lane, int q0, int w0r,
                                          int no, int nc, int R, int CR, uint32_t magic_cr, uint32_t magic) {
@@ -387,8 +408,10 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, i
   uint32_t off[K];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
-    const int c = lane + 64 * k;
-    if (c < chunks) {
+    // (unconditional, inside the wave's stage: a read under `c < chunks` became a branch with
+    // its own wait, the three reads one after another)
+    const int c = WAB2_COPY_UNCOND ? min(lane + 64 * k, 32 * CR - 1) : lane + 64 * k;
+    if (WAB2_COPY_UNCOND || c < chunks) {
       const int r = (int)(((uint32_t)c * magic_cr) >> 16);  // stage slot: c / CR
       const int qq = q0 + r;
       const int ww = (int)(((uint32_t)qq * magic) >> 20);
@@ -396,9 +419,35 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, i
       val[k] = *reinterpret_cast<const u32x4*>(stage + 16 * c);
     }
   }
+  // (all reads issued, then one wait: the compiler otherwise sank the last read into its store's
+  // branch)
+  if (WAB2_COPY_UNCOND)
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) asm volatile("" : "+v"(val[k]));
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (lane + 64 * k < chunks) __builtin_nontemporal_store(val[k], reinterpret_cast<u32x4*>(rbase + off[k]));
+}
+
+// NW dwords xs[] into the record stage at dword D0 of a record of RDW dwords, in the widest
+// aligned writes (8 / 16 bytes; zeros past NW where the record's pad allows): a bush round's
+// records are written by 32 lanes at stride R, so every write instruction is bank-conflicted
+// alike and fewer, wider ones take fewer LDS cycles
+template <int D0, int NW, int RDW>
+__device__ __forceinline__ void put_dwords(uint8_t* rec, const uint32_t* xs) {
+  if constexpr (NW > 0) {
+    if constexpr (D0 % 4 == 0 && (NW >= 4 || D0 + 4 <= RDW)) {
+      *reinterpret_cast<uint4*>(rec + 4 * D0) = make_uint4(xs[0], NW > 1 ? xs[NW > 1 ? 1 : 0] : 0u, NW > 2 ? xs[NW > 2 ? 2 : 0] : 0u,
+                                                           NW > 3 ? xs[NW > 3 ? 3 : 0] : 0u);
+      put_dwords<D0 + 4, (NW > 4 ? NW - 4 : 0), RDW>(rec, xs + (NW > 4 ? 4 : 0));
+    } else if constexpr (D0 % 2 == 0 && (NW >= 2 || D0 + 2 <= RDW)) {
+      *reinterpret_cast<uint2*>(rec + 4 * D0) = make_uint2(xs[0], NW > 1 ? xs[NW > 1 ? 1 : 0] : 0u);
+      put_dwords<D0 + 2, (NW > 2 ? NW - 2 : 0), RDW>(rec, xs + (NW > 2 ? 2 : 0));
+    } else {
+      *reinterpret_cast<uint32_t*>(rec + 4 * D0) = xs[0];
+      put_dwords<D0 + 1, NW - 1, RDW>(rec, xs + (NW > 1 ? 1 : 0));
+    }
+  }
 }
 
 // NKK = ceil(N / 4): dword-pair groups of the delta array.  CNO, CNW, CNB > 0: an instance for
@@ -700,13 +749,21 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
                 if (kFixed) {
+                  uint32_t xs[kRowW];
 #pragma unroll
                   for (int k = 0; k < kRowW; ++k) {
-                    if (WAB2_ABLATE & 4) break;
                     uint32_t x = rdw[k];
                     if (sh) x = (x << (8 * sh)) | (k > 0 ? rdw[k > 0 ? k - 1 : 0] >> (32 - 8 * sh) : 0u);
                     const uint32_t b4 = (uint32_t)(v64 >> (NM + 4 * k - sh + 8)) & 0xFu;
-                    *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                    xs[k] = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                  }
+                  if (!(WAB2_ABLATE & 4)) {
+                    if (WAB2_BUSH_WIDE) {
+                      put_dwords<kFixed ? (24 + 2 * kN) / 4 : 0, kRowW, kFixed ? (24 + 2 * kN + CNB + 15) / 16 * 4 : 0>(rec, xs);
+                    } else {
+#pragma unroll
+                      for (int k = 0; k < kRowW; ++k) *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = xs[k];
+                    }
                   }
                 } else
                 for (int k = 0; k < ((WAB2_ABLATE & 4) ? 0 : ndw); ++k) {
@@ -819,7 +876,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             }
 #endif
           }
-          vis |= __shfl_xor(vis, 32);
+          if (kFixed && WAB2_DELTA_B64) {  // (the other half's bits by a half swap, not an LDS permute)
+            const auto r = __builtin_amdgcn_permlane32_swap(vis, vis, false, false);
+            vis |= hf ? r[0] : r[1];
+          } else {
+            vis |= __shfl_xor(vis, 32);
+          }
           // internal obs (World.py:17-18, 50-51, 80-81)
           double food;
           int x, y;
@@ -845,7 +907,22 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             // in full, and nothing writes the pad non-zero; the stage is zeroed each turn)
             for (int z = (bb + 2 * nbp + 3) & ~3; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
           }
-          if (!bush) {  // (a bush's deltas are zero: the stage's, since the turn's first round)
+          if (!bush && kFixed && WAB2_DELTA_B64) {
+            // delta dwords in pairs: one v_permlane32_swap of d[kk], d[kk + 1] gives the lower
+            // half dwords 2kk, 2kk + 1 and the upper half 2kk + 2, 2kk + 3, each one 8-byte
+            // stage write (half the writes of 32 records at stride R, each as bank-conflicted)
+#pragma unroll
+            for (int kk = 0; kk < NKK; kk += 2) {
+              if (kk + 1 < NKK) {
+                const auto r = __builtin_amdgcn_permlane32_swap(d[kk], d[kk + 1], false, false);
+                const int k0 = 2 * kk + 2 * hf;
+                if (k0 + 1 < nd) *reinterpret_cast<uint2*>(rec + 24 + 4 * k0) = make_uint2(r[0], r[1]);
+                else if (k0 < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * k0) = r[0];
+              } else if (2 * kk + hf < nd) {
+                *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+              }
+            }
+          } else if (!bush) {  // (a bush's deltas are zero: the stage's, since the turn's first round)
 #pragma unroll
             for (int kk = 0; kk < NKK; ++kk)
               if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
@@ -868,7 +945,29 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
             }
           }
-          for (int m = hf; m < ((bush || (WAB2_ABLATE & 4)) ? 0 : nbp); m += 2) {
+          // (the fixed instance with a 16-byte row: the row in one ds_read_b128, its byte pairs
+          // m = 2mm + half by shifts; the loop below waited for each pair's read in turn)
+          constexpr bool kRow128 = kFixed && WAB2_MOVER_ROW128 && CNB % 4 == 0 && CNB <= 16 && ((CNB + 3) & ~3) == 16;
+          if (kRow128 && !bush && !(WAB2_ABLATE & 4)) {
+            const u32x4 rv = *reinterpret_cast<const u32x4*>((type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp);
+#pragma unroll
+            for (int mm = 0; mm < (kRow128 ? CNB / 4 : 0); ++mm) {
+              const int b = 4 * mm + 2 * hf;
+              uint32_t f = (rv[mm] >> (16 * hf)) & 0xFFFFu;
+              if (type == T_OSTRICH) {
+                for (int k = a0; k < min(a1, NO); ++k)
+                  if (k < i) {
+                    const uint32_t e = s.ev[k * kWorlds + w];
+                    if ((e & 0xFFu) == (uint32_t)b) f = (f & 0xFF00u) | (e >> 8);
+                    if ((e & 0xFFu) == (uint32_t)b + 1u) f = (f & 0x00FFu) | (e & 0xFF00u);
+                  }
+              }
+              const uint32_t vb = vis >> (NM + b);
+              f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
+              *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
+            }
+          }
+          for (int m = hf; m < ((kRow128 || bush || (WAB2_ABLATE & 4)) ? 0 : nbp); m += 2) {
             const int b = 2 * m;
             const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
             uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
@@ -951,13 +1050,21 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
                 if (kFixed) {
+                  uint32_t xs[kRowW];
 #pragma unroll
                   for (int k = 0; k < kRowW; ++k) {
-                    if (WAB2_ABLATE & 4) break;
                     uint32_t x = rdw[k];
                     if (sh) x = (x << (8 * sh)) | (k > 0 ? rdw[k > 0 ? k - 1 : 0] >> (32 - 8 * sh) : 0u);
                     const uint32_t b4 = (uint32_t)(v64 >> (NM + 4 * k - sh + 8)) & 0xFu;
-                    *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                    xs[k] = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+                  }
+                  if (!(WAB2_ABLATE & 4)) {
+                    if (WAB2_BUSH_WIDE) {
+                      put_dwords<kFixed ? (24 + 2 * kN) / 4 : 0, kRowW, kFixed ? (24 + 2 * kN + CNB + 15) / 16 * 4 : 0>(rec, xs);
+                    } else {
+#pragma unroll
+                      for (int k = 0; k < kRowW; ++k) *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = xs[k];
+                    }
                   }
                 } else
                 for (int k = 0; k < ((WAB2_ABLATE & 4) ? 0 : ndw); ++k) {
