@@ -387,6 +387,9 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
 #ifndef WAB2_BUSH_WIDE  // (tuning A/B: 0 = a bush record's food dwords one by one)
 #define WAB2_BUSH_WIDE 1
 #endif
+#ifndef WAB2_MOVER_CHUNKS  // (tuning A/B: 0 = a mover record's fields written one by one)
+#define WAB2_MOVER_CHUNKS 1
+#endif
 #ifndef WAB2_MOVER_ROW128  // (tuning A/B: 0 = a mover round's bush-food pairs read one by one)
 #define WAB2_MOVER_ROW128 1
 #endif
@@ -437,8 +440,8 @@ template <int D0, int NW, int RDW>
 __device__ __forceinline__ void put_dwords(uint8_t* rec, const uint32_t* xs) {
   if constexpr (NW > 0) {
     if constexpr (D0 % 4 == 0 && (NW >= 4 || D0 + 4 <= RDW)) {
-      *reinterpret_cast<uint4*>(rec + 4 * D0) = make_uint4(xs[0], NW > 1 ? xs[NW > 1 ? 1 : 0] : 0u, NW > 2 ? xs[NW > 2 ? 2 : 0] : 0u,
-                                                           NW > 3 ? xs[NW > 3 ? 3 : 0] : 0u);
+      *reinterpret_cast<u32x4*>(rec + 4 * D0) = (u32x4){xs[0], NW > 1 ? xs[NW > 1 ? 1 : 0] : 0u, NW > 2 ? xs[NW > 2 ? 2 : 0] : 0u,
+                                                        NW > 3 ? xs[NW > 3 ? 3 : 0] : 0u};
       put_dwords<D0 + 4, (NW > 4 ? NW - 4 : 0), RDW>(rec, xs + (NW > 4 ? 4 : 0));
     } else if constexpr (D0 % 2 == 0 && (NW >= 2 || D0 + 2 <= RDW)) {
       *reinterpret_cast<uint2*>(rec + 4 * D0) = make_uint2(xs[0], NW > 1 ? xs[NW > 1 ? 1 : 0] : 0u);
@@ -744,7 +747,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               if (q0 >= nitems) break;  // (uniform)
               if (hf == half) {
                 uint8_t* rec = stage + (lane & 31) * R;
-                *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8);
+                *reinterpret_cast<u32x4*>(rec) = (u32x4){(uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8};
                 *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, (uint32_t)T_BUSH << 16);
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
@@ -898,63 +901,120 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           }
           const uint32_t flags = type == T_OSTRICH ? (uint32_t)role | ((uint32_t)status << 8) : 0u;
           uint8_t* rec = stage + (lane & 31) * R;
-          if (hf == 0) {
-            const uint64_t fb = (uint64_t)__double_as_longlong(food);
-            *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
-            *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
-          } else if (!bush) {
-            // (only the pad past the bush-food bytes: the deltas and those bytes are written below
-            // in full, and nothing writes the pad non-zero; the stage is zeroed each turn)
-            for (int z = (bb + 2 * nbp + 3) & ~3; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
-          }
-          if (!bush && kFixed && WAB2_DELTA_B64) {
-            // delta dwords in pairs: one v_permlane32_swap of d[kk], d[kk + 1] gives the lower
-            // half dwords 2kk, 2kk + 1 and the upper half 2kk + 2, 2kk + 3, each one 8-byte
-            // stage write (half the writes of 32 records at stride R, each as bank-conflicted)
+          // (the benched geometry, 25 entities and 16 bushes in 96-byte records: each lane writes
+          // three whole 16-byte chunks of its item's record, the lower half chunks 0, 2, 4 and the
+          // upper half 1, 3, 5, the delta dwords exchanged between the halves by three
+          // v_permlane32_swap: three stage writes per lane instead of about ten narrow ones, each
+          // a write of 32 records at stride 96 B, as bank-conflicted whatever its width)
+          constexpr bool kChunks = kFixed && WAB2_MOVER_CHUNKS && kN == 25 && CNB == 16 && NKK == 7;
+          if (kChunks && !bush) {
+            const u32x4 rv = *reinterpret_cast<const u32x4*>((type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp);
+            uint32_t F[4] = {rv[0], rv[1], rv[2], rv[3]};  // bush food bytes 4q .. 4q + 3
+            if (type == T_OSTRICH) {  // (the eats of the ostriches that acted before i)
+              for (int k = a0; k < min(a1, NO); ++k)
+                if (k < i) {
+                  const uint32_t e = s.ev[k * kWorlds + w], b = e & 0xFFu, sb = 8u * (b & 3u);
 #pragma unroll
-            for (int kk = 0; kk < NKK; kk += 2) {
-              if (kk + 1 < NKK) {
-                const auto r = __builtin_amdgcn_permlane32_swap(d[kk], d[kk + 1], false, false);
-                const int k0 = 2 * kk + 2 * hf;
-                if (k0 + 1 < nd) *reinterpret_cast<uint2*>(rec + 24 + 4 * k0) = make_uint2(r[0], r[1]);
-                else if (k0 < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * k0) = r[0];
-              } else if (2 * kk + hf < nd) {
-                *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+                  for (int q = 0; q < 4; ++q)
+                    if ((b >> 2) == (uint32_t)q) F[q] = (F[q] & ~(0xFFu << sb)) | (((e >> 8) & 0xFFu) << sb);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t b4 = (vis >> (NM + 4 * q)) & 0xFu;
+              F[q] &= ((WAB2_ABLATE & 4) ? 0u : ~0u) & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+            }
+            // a' = {lo: a lo, hi: b lo}, b' = {lo: a hi, hi: b hi}: delta dword k = 2kk + half
+            const auto S1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);  // k 2, 3 | 6, 7
+            const auto S2 = __builtin_amdgcn_permlane32_swap(d[2], d[4], false, false);  // k 4, 5 | 8, 9
+            const auto S3 = __builtin_amdgcn_permlane32_swap(d[5], d[0], false, false);  // k 10, 11 | 0, 1
+            const uint64_t fb = (uint64_t)__double_as_longlong(food);
+            // bytes 72-75: entity 24's delta (the lower half's d[6]; entity 25 is absent) and
+            // bush-food bytes 0-1 from byte 74; the rest of the bush food to byte 89, then pad
+            const uint32_t dw18 = d[6] | (F[0] << 16), dw19 = (F[0] >> 16) | (F[1] << 16);
+            const uint32_t dw20 = (F[1] >> 16) | (F[2] << 16), dw21 = (F[2] >> 16) | (F[3] << 16), dw22 = F[3] >> 16;
+            const uint32_t ft = flags | ((uint32_t)type << 16);
+            const u32x4 c1 = hf ? (u32x4){vis, ft, S3[0], S3[1]} : (u32x4){(uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y};
+            const u32x4 c2 = (u32x4){S1[0], S1[1], S2[0], S2[1]};
+            const u32x4 c3 = hf ? (u32x4){dw20, dw21, dw22, 0u} : (u32x4){S3[0], S3[1], dw18, dw19};
+            *reinterpret_cast<u32x4*>(rec + 16 * hf) = c1;
+            *reinterpret_cast<u32x4*>(rec + 32 + 16 * hf) = c2;
+            *reinterpret_cast<u32x4*>(rec + 64 + 16 * hf) = c3;
+          } else {
+            if (hf == 0) {
+              const uint64_t fb = (uint64_t)__double_as_longlong(food);
+              *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), (uint32_t)x, (uint32_t)y);
+              *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, flags | ((uint32_t)type << 16));
+            } else if (!bush) {
+              // (only the pad past the bush-food bytes: the deltas and those bytes are written below
+              // in full, and nothing writes the pad non-zero; the stage is zeroed each turn)
+              for (int z = (bb + 2 * nbp + 3) & ~3; z < R; z += 4) *reinterpret_cast<uint32_t*>(rec + z) = 0u;
+            }
+            if (!bush && kFixed && WAB2_DELTA_B64) {
+              // delta dwords in pairs: one v_permlane32_swap of d[kk], d[kk + 1] gives the lower
+              // half dwords 2kk, 2kk + 1 and the upper half 2kk + 2, 2kk + 3, each one 8-byte
+              // stage write (half the writes of 32 records at stride R, each as bank-conflicted)
+  #pragma unroll
+              for (int kk = 0; kk < NKK; kk += 2) {
+                if (kk + 1 < NKK) {
+                  const auto r = __builtin_amdgcn_permlane32_swap(d[kk], d[kk + 1], false, false);
+                  const int k0 = 2 * kk + 2 * hf;
+                  if (k0 + 1 < nd) *reinterpret_cast<uint2*>(rec + 24 + 4 * k0) = make_uint2(r[0], r[1]);
+                  else if (k0 < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * k0) = r[0];
+                } else if (2 * kk + hf < nd) {
+                  *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+                }
+              }
+            } else if (!bush) {  // (a bush's deltas are zero: the stage's, since the turn's first round)
+  #pragma unroll
+              for (int kk = 0; kk < NKK; ++kk)
+                if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
+            }
+            // Additional_Data [food] of the visible bushes as the observer sees them: after the
+            // eats of the ostriches that acted before it in this launch (bf1 for every observer
+            // after the ostriches); byte pairs m = 2mm + half
+            if (bush && !(WAB2_ABLATE & 4)) {
+              // a bush sees bf1; its record's bytes around the bush-food ones are zero (deltas,
+              // tail), so the region goes out as whole dwords from bb & ~3: dword k holds bushes
+              // 4k - sh .. 4k - sh + 3, masked by their visibility bits
+              const uint8_t* row = s.bf1 + w * NBp;
+              const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
+              const uint64_t v64 = (uint64_t)vis << 8;  // (bit NM + b + 8: bush b, b >= -8)
+              for (int k = hf; k < ndw; k += 2) {
+                const int b = 4 * k - sh;
+                uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
+                if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
+                const uint32_t b4 = (uint32_t)(v64 >> (NM + b + 8)) & 0xFu;
+                *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
               }
             }
-          } else if (!bush) {  // (a bush's deltas are zero: the stage's, since the turn's first round)
-#pragma unroll
-            for (int kk = 0; kk < NKK; ++kk)
-              if (2 * kk + hf < nd) *reinterpret_cast<uint32_t*>(rec + 24 + 4 * (2 * kk + hf)) = d[kk];
-          }
-          // Additional_Data [food] of the visible bushes as the observer sees them: after the
-          // eats of the ostriches that acted before it in this launch (bf1 for every observer
-          // after the ostriches); byte pairs m = 2mm + half
-          if (bush && !(WAB2_ABLATE & 4)) {
-            // a bush sees bf1; its record's bytes around the bush-food ones are zero (deltas,
-            // tail), so the region goes out as whole dwords from bb & ~3: dword k holds bushes
-            // 4k - sh .. 4k - sh + 3, masked by their visibility bits
-            const uint8_t* row = s.bf1 + w * NBp;
-            const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
-            const uint64_t v64 = (uint64_t)vis << 8;  // (bit NM + b + 8: bush b, b >= -8)
-            for (int k = hf; k < ndw; k += 2) {
-              const int b = 4 * k - sh;
-              uint32_t x = *reinterpret_cast<const uint32_t*>(row + 4 * k);
-              if (sh) x = (x << 16) | (k > 0 ? *reinterpret_cast<const uint32_t*>(row + 4 * k - 4) >> 16 : 0u);
-              const uint32_t b4 = (uint32_t)(v64 >> (NM + b + 8)) & 0xFu;
-              *reinterpret_cast<uint32_t*>(rec + 4 * (d0 + k)) = x & (((b4 * 0x00204081u) & 0x01010101u) * 0xFFu);
+            // (the fixed instance with a 16-byte row: the row in one ds_read_b128, its byte pairs
+            // m = 2mm + half by shifts; the loop below waited for each pair's read in turn)
+            constexpr bool kRow128 = kFixed && WAB2_MOVER_ROW128 && CNB % 4 == 0 && CNB <= 16 && ((CNB + 3) & ~3) == 16;
+            if (kRow128 && !bush && !(WAB2_ABLATE & 4)) {
+              const u32x4 rv = *reinterpret_cast<const u32x4*>((type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp);
+  #pragma unroll
+              for (int mm = 0; mm < (kRow128 ? CNB / 4 : 0); ++mm) {
+                const int b = 4 * mm + 2 * hf;
+                uint32_t f = (rv[mm] >> (16 * hf)) & 0xFFFFu;
+                if (type == T_OSTRICH) {
+                  for (int k = a0; k < min(a1, NO); ++k)
+                    if (k < i) {
+                      const uint32_t e = s.ev[k * kWorlds + w];
+                      if ((e & 0xFFu) == (uint32_t)b) f = (f & 0xFF00u) | (e >> 8);
+                      if ((e & 0xFFu) == (uint32_t)b + 1u) f = (f & 0x00FFu) | (e & 0xFF00u);
+                    }
+                }
+                const uint32_t vb = vis >> (NM + b);
+                f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
+                *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
+              }
             }
-          }
-          // (the fixed instance with a 16-byte row: the row in one ds_read_b128, its byte pairs
-          // m = 2mm + half by shifts; the loop below waited for each pair's read in turn)
-          constexpr bool kRow128 = kFixed && WAB2_MOVER_ROW128 && CNB % 4 == 0 && CNB <= 16 && ((CNB + 3) & ~3) == 16;
-          if (kRow128 && !bush && !(WAB2_ABLATE & 4)) {
-            const u32x4 rv = *reinterpret_cast<const u32x4*>((type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp);
-#pragma unroll
-            for (int mm = 0; mm < (kRow128 ? CNB / 4 : 0); ++mm) {
-              const int b = 4 * mm + 2 * hf;
-              uint32_t f = (rv[mm] >> (16 * hf)) & 0xFFFFu;
-              if (type == T_OSTRICH) {
+            for (int m = hf; m < ((kRow128 || bush || (WAB2_ABLATE & 4)) ? 0 : nbp); m += 2) {
+              const int b = 2 * m;
+              const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
+              uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
+              if (!bush && type == T_OSTRICH) {
                 for (int k = a0; k < min(a1, NO); ++k)
                   if (k < i) {
                     const uint32_t e = s.ev[k * kWorlds + w];
@@ -966,22 +1026,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
               *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
             }
-          }
-          for (int m = hf; m < ((kRow128 || bush || (WAB2_ABLATE & 4)) ? 0 : nbp); m += 2) {
-            const int b = 2 * m;
-            const uint8_t* row = (type == T_OSTRICH ? s.bf0 : s.bf1) + w * NBp;
-            uint32_t f = *reinterpret_cast<const uint16_t*>(row + b);
-            if (!bush && type == T_OSTRICH) {
-              for (int k = a0; k < min(a1, NO); ++k)
-                if (k < i) {
-                  const uint32_t e = s.ev[k * kWorlds + w];
-                  if ((e & 0xFFu) == (uint32_t)b) f = (f & 0xFF00u) | (e >> 8);
-                  if ((e & 0xFFu) == (uint32_t)b + 1u) f = (f & 0x00FFu) | (e & 0xFF00u);
-                }
-            }
-            const uint32_t vb = vis >> (NM + b);
-            f &= ((vb & 1u) ? 0x00FFu : 0u) | ((b + 1 < NB && (vb & 2u)) ? 0xFF00u : 0u);
-            *reinterpret_cast<uint16_t*>(rec + bb + b) = (uint16_t)f;
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1045,7 +1089,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               if (q0 >= nitems) break;  // (uniform)
               if (hf == half) {
                 uint8_t* rec = stage + (lane & 31) * R;
-                *reinterpret_cast<uint4*>(rec) = make_uint4((uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8);
+                *reinterpret_cast<u32x4*>(rec) = (u32x4){(uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8};
                 *reinterpret_cast<uint2*>(rec + 16) = make_uint2(vis, (uint32_t)T_BUSH << 16);
                 // the bush-food bytes as whole dwords from bb & ~3 (the record's bytes around them
                 // are zero: deltas, tail): dword k holds bushes 4k - sh .. 4k - sh + 3
