@@ -387,12 +387,30 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
 #ifndef WAB2_BUSH_WIDE  // (tuning A/B: 0 = a bush record's food dwords one by one)
 #define WAB2_BUSH_WIDE 1
 #endif
+#ifndef WAB2_STORE_THROTTLE  // (vmcnt(N) at each mover round's start; -1: none)
+#define WAB2_STORE_THROTTLE 0
+#endif
+#ifndef WAB2_BUSH_THROTTLE  // (tuning A/B: 1 = vmcnt(0) also before a bush round's second half)
+#define WAB2_BUSH_THROTTLE 0
+#endif
+#ifndef WAB2_POST_THROTTLE  // (tuning A/B: 1 = vmcnt(0) right after every copy-out)
+#define WAB2_POST_THROTTLE 0
+#endif
 #ifndef WAB2_MOVER_CHUNKS  // (tuning A/B: 0 = a mover record's fields written one by one)
 #define WAB2_MOVER_CHUNKS 1
 #endif
 #ifndef WAB2_MOVER_ROW128  // (tuning A/B: 0 = a mover round's bush-food pairs read one by one)
 #define WAB2_MOVER_ROW128 1
 #endif
+#ifndef WAB2_REC_NT  // (tuning A/B: 0 = plain record stores)
+#define WAB2_REC_NT 1
+#endif
+__device__ __forceinline__ void rec_store(u32x4 v, u32x4* dst) {
+  if (WAB2_REC_NT)
+    __builtin_nontemporal_store(v, dst);
+  else
+    *dst = v;
+}
 template <int KMAX>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, int chunks, int lane, int q0, int w0r,
                                          int no, int nc, int R, int CR, uint32_t magic_cr, uint32_t magic) {
@@ -402,7 +420,7 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, i
       const int qq = q0 + r;
       const int ww = (int)(((uint32_t)qq * magic) >> 20);
       const uint32_t off = (uint32_t)(((ww - w0r) * no + (qq - ww * nc)) * R + 16 * (c - r * CR));
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(stage + 16 * c), reinterpret_cast<u32x4*>(rbase + off));
+      rec_store(*reinterpret_cast<const u32x4*>(stage + 16 * c), reinterpret_cast<u32x4*>(rbase + off));
     }
     return;
   }
@@ -429,7 +447,7 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, uint8_t* rbase, i
     for (int k = 0; k < KMAX; ++k) asm volatile("" : "+v"(val[k]));
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
-    if (lane + 64 * k < chunks) __builtin_nontemporal_store(val[k], reinterpret_cast<u32x4*>(rbase + off[k]));
+    if (lane + 64 * k < chunks) rec_store(val[k], reinterpret_cast<u32x4*>(rbase + off[k]));
 }
 
 // NW dwords xs[] into the record stage at dword D0 of a record of RDW dwords, in the widest
@@ -745,6 +763,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             for (int half = 0; half < 2; ++half) {
               const int q0 = rnd * 64 + 32 * half;
               if (q0 >= nitems) break;  // (uniform)
+#if WAB2_BUSH_THROTTLE
+              if (half) __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
               if (hf == half) {
                 uint8_t* rec = stage + (lane & 31) * R;
                 *reinterpret_cast<u32x4*>(rec) = (u32x4){(uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8};
@@ -783,6 +804,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               const int w0r = (int)(((uint32_t)q0 * magic_b) >> 20);
               uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;
               copy_out<kCopyMax>(stage, rbase, (WAB2_ABLATE & 2) ? 0 : chunks, lane, q0, w0r, no, nc, R, CR, magic_cr, magic_b);
+#if WAB2_POST_THROTTLE
+              __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
               __builtin_amdgcn_wave_barrier();
             }
           }
@@ -799,6 +823,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const uint32_t magic = bush ? magic_b : magic_m;  // q / nc = (q * magic) >> 20
         const int nitems = (WAB2_ABLATE & (bush ? 16 : 32)) ? 0 : nvalid * nc;
         for (int rnd = wave; rnd * 32 < nitems; rnd += 4) {
+          // (tuning A/B: cap the wave's record stores in flight at a mover round's start)
+#if WAB2_STORE_THROTTLE >= 0
+          __builtin_amdgcn_s_waitcnt((WAB2_STORE_THROTTLE & 15) | ((WAB2_STORE_THROTTLE >> 4) << 14) | 0x0F70);
+#endif
           const int q = rnd * 32 + (lane & 31);
           const bool on = q < nitems;
           const int qc = on ? q : nitems - 1;  // (lanes past the last item compute a copy of it)
@@ -1037,6 +1065,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int w0r = (int)(((uint32_t)q0 * magic) >> 20);  // the round's first world
           uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;  // its first record
           copy_out<kCopyMax>(stage, rbase, (WAB2_ABLATE & 2) ? 0 : chunks, lane, q0, w0r, no, nc, R, CR, magic_cr, magic);
+#if WAB2_POST_THROTTLE
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
           __builtin_amdgcn_wave_barrier();
         }
       }
@@ -1087,6 +1118,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             for (int half = 0; half < 2; ++half) {
               const int q0 = rnd * 64 + 32 * half;
               if (q0 >= nitems) break;  // (uniform)
+#if WAB2_BUSH_THROTTLE
+              if (half) __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
               if (hf == half) {
                 uint8_t* rec = stage + (lane & 31) * R;
                 *reinterpret_cast<u32x4*>(rec) = (u32x4){(uint32_t)fb, (uint32_t)(fb >> 32), bxy & 0xFFu, bxy >> 8};
@@ -1125,6 +1159,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
               const int w0r = (int)(((uint32_t)q0 * magic_b) >> 20);
               uint8_t* rbase = obs_t + (item0 + (int64_t)w0r * no + (c0 - o0)) * R;
               copy_out<kCopyMax>(stage, rbase, (WAB2_ABLATE & 2) ? 0 : chunks, lane, q0, w0r, no, nc, R, CR, magic_cr, magic_b);
+#if WAB2_POST_THROTTLE
+              __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
               __builtin_amdgcn_wave_barrier();
             }
           }
