@@ -402,8 +402,10 @@ __device__ __forceinline__ uint32_t view_pair2(const View2& v, uint32_t xy, uint
 #ifndef WAB2_MOVER_ROW128  // (tuning A/B: 0 = a mover round's bush-food pairs read one by one)
 #define WAB2_MOVER_ROW128 1
 #endif
-#ifndef WAB2_REC_NT  // (tuning A/B: 0 = plain record stores)
-#define WAB2_REC_NT 1
+// Record stores plain, not non-temporal: 46.77-46.89 -> 44.76-44.86 us per turn on one box
+// (the per-step gym kernel measured the opposite for its obs stores)
+#ifndef WAB2_REC_NT  // (tuning A/B: 1 = non-temporal record stores)
+#define WAB2_REC_NT 0
 #endif
 __device__ __forceinline__ void rec_store(u32x4 v, u32x4* dst) {
   if (WAB2_REC_NT)
