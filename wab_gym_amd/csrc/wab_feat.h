@@ -194,7 +194,11 @@ constexpr int kFeatStoreUnroll = 4;
 __device__ __forceinline__ void nt_store_f4(const float4& f, float4* dst) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   const f32x4 v = {f.x, f.y, f.z, f.w};
-  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+#ifndef WAB_FEAT_NT  // (tuning A/B: 0 = plain feature stores)
+#define WAB_FEAT_NT 1
+#endif
+  if (WAB_FEAT_NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+  else *reinterpret_cast<f32x4*>(dst) = v;
 }
 
 // (NT: non-temporal stores)

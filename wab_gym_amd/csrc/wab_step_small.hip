@@ -36,6 +36,9 @@
 
 #include "wab_feat.h"
 
+#ifndef WAB_ROLL_OBS_NT  // (tuning A/B: 0 = plain obs stores in multi-step launches)
+#define WAB_ROLL_OBS_NT 1
+#endif
 namespace wab {
 
 // Diagnostic build (-DWAB_STAMPS): lane 0 of each wave records s_memrealtime (100 MHz) at
@@ -426,7 +429,8 @@ __device__ __forceinline__ void store_units_nt(const Params& p, uint8_t* planes,
     u32x4 q;
 #pragma unroll
     for (int b = 0; b < 4; ++b) q[b] = (((v[k] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    if (WAB_ROLL_OBS_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    else reinterpret_cast<u32x4*>(out)[u] = q;
   }
 }
 
@@ -1365,7 +1369,8 @@ __device__ __forceinline__ void store_units_of(const Params& p, uint32_t* stream
     u32x4 q;
 #pragma unroll
     for (int b = 0; b < 4; ++b) q[b] = (((v[k - K0] >> (4 * b)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    if (WAB_ROLL_OBS_NT) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out) + u);
+    else reinterpret_cast<u32x4*>(out)[u] = q;
   }
 }
 

@@ -183,6 +183,13 @@ __device__ __forceinline__ void copy_to_lds(T* dst, const T* src, int n, int lan
 }
 
 // 16 cells of one row -> 16 bytes
+#ifndef WAB_WIDE_OBS_NT  // (tuning A/B: 0 = plain obs stores)
+#define WAB_WIDE_OBS_NT 1
+#endif
+__device__ __forceinline__ void wide_obs_store(u32x4 v, u32x4* dst) {
+  if (WAB_WIDE_OBS_NT) __builtin_nontemporal_store(v, dst);
+  else *dst = v;
+}
 __device__ __forceinline__ u32x4 expand16(uint32_t v) {
   u32x4 q;
 #pragma unroll
@@ -1045,7 +1052,7 @@ __device__ __forceinline__ void store_block(const Params& p, const RowQueue& q, 
   const uint32_t k = (rr >= W ? 1u : 0u) + (rr >= 2u * W ? 1u : 0u);
   const uint32_t i = rr - k * W;
   const uint32_t v = k == 2u ? (i == (uint32_t)p.cw ? 1u << p.ch : 0u) : (k == 0u ? q.wp : q.bm)[e * kRollPitch + i];
-  __builtin_nontemporal_store(expand16((v >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(q.out) + e * CPE + rr * CPR + half);
+  wide_obs_store(expand16((v >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(q.out) + e * CPE + rr * CPR + half);
 }
 
 // The last step's ostrich-plane lines: the plane is the centre cell alone, the same in every
@@ -1069,7 +1076,7 @@ __device__ __forceinline__ bool drain_plane2(const Params& p, uint32_t* ctr, int
     if (ch < z) {
       const uint32_t o = ch - base, rr = CPR == 2u ? o >> 1 : o, half = CPR == 2u ? o & 1u : 0u;
       const uint32_t v2 = rr - 2u * W == (uint32_t)p.cw ? 1u << p.ch : 0u;
-      __builtin_nontemporal_store(expand16((v2 >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(out) + ch);
+      wide_obs_store(expand16((v2 >> (16u * half)) & 0xFFFFu), reinterpret_cast<u32x4*>(out) + ch);
     }
   }
 }

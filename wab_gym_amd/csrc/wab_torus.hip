@@ -718,7 +718,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       // 50.61 µs per turn; by workgroup instead of by wave 50.88).  A bush round writes only its
       // headers and bush bytes into a stage that is zero elsewhere: after mover rounds the
       // wave's stage is zeroed again.
-      const bool movers_first = wave >= 2;
+#ifndef WAB2_ORDER  // (tuning A/B: 0 = waves 2-3 movers first; 1 = every wave movers first; 2 = bushes first)
+#define WAB2_ORDER 0
+#endif
+      const bool movers_first = WAB2_ORDER == 0 ? wave >= 2 : WAB2_ORDER == 1;
       if (!movers_first) {
         // ---- the bush observers: one lane per (world, bush) item, 64 items per round, their
         // records staged and stored in two halves of 32
