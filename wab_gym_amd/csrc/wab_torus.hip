@@ -721,7 +721,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
 #ifndef WAB2_ORDER  // (tuning A/B: 0 = waves 2-3 movers first; 1 = every wave movers first; 2 = bushes first)
 #define WAB2_ORDER 0
 #endif
-      const bool movers_first = WAB2_ORDER == 0 ? wave >= 2 : WAB2_ORDER == 1;
+      const bool movers_first = WAB2_ORDER == 0 ? wave >= 2 : WAB2_ORDER == 3 ? wave >= 1 : WAB2_ORDER == 4 ? wave >= 3 : WAB2_ORDER == 1;
       if (!movers_first) {
         // ---- the bush observers: one lane per (world, bush) item, 64 items per round, their
         // records staged and stored in two halves of 32
