@@ -256,6 +256,9 @@ __device__ __forceinline__ TParams kparams(const TParams& p0) {
 #endif
 }
 
+#ifndef WAB2_ACT_LATE  // (tuning A/B: 1 = the next turn's actions fetched by W3 at the end of phase B; measured slower)
+#define WAB2_ACT_LATE 0
+#endif
 #ifndef WAB2_ACT_DRAIN  // (tuning A/B: 1 = drain the action loads; measured slower, below)
 #define WAB2_ACT_DRAIN 0
 #endif
@@ -679,7 +682,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         const uint32_t np = (uint32_t)wrap1((int)(bxy & 0xFFu), W) | ((uint32_t)wrap1((int)(bxy >> 8), H) << 8);
         reinterpret_cast<uint16_t*>(s.pos + w * Np + NM + b)[1] = (uint16_t)np;
       }
-    } else if (t + 1 < T) {
+    } else if (t + 1 < T && !(WAB2_ACT_LATE && kFixed)) {
       WAB2_PHASE_PARAMS;
       fetch_actions_wave(p, t + 1, wg0, nvalid, (t & 1) ? s.act0 : s.act1, lane);
     }
@@ -1173,6 +1176,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
         }
       }
       WAB2_STAMP(4);
+      // the next turn's actions, by W3 at the end of its rounds (it reaches the phase-B barrier
+      // with the most slack, and the fetch's HBM round trip was the longest part of phase A);
+      // the buffer is the one turn t - 1 used, read last in its phase C
+      if (WAB2_ACT_LATE && kFixed && wave == 3 && t + 1 < T) fetch_actions_wave(p, t + 1, wg0, nvalid, (t & 1) ? s.act0 : s.act1, lane);
       // reward and done of a whole turn's (world, entity) items (compute_reward World.py:21-22,
       // 54-58, 84-85; is_entity_done :339-343), from the tables as the observers saw them (phase
       // C updates them after the barrier): the workgroup's [64][N] slice of [B][N] is contiguous,
