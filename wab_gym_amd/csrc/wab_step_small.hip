@@ -36,6 +36,9 @@
 
 #include "wab_feat.h"
 
+#ifndef WAB_ROLL_THROTTLE  // (tuning A/B: 1 = W0 / W2 drain their obs stores at each step's start)
+#define WAB_ROLL_THROTTLE 0
+#endif
 #ifndef WAB_ROLL_OBS_NT  // (tuning A/B: 0 = plain obs stores in multi-step launches)
 #define WAB_ROLL_OBS_NT 1
 #endif
@@ -1609,6 +1612,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROLL ? 4 : 
 #define WAB_ROLL_STEP(...)                                                                   \
     for (int t = 0; t < T; ++t) {                                                            \
       ROLL_LOOP_STAMP(35, t == T / 2);  /* the middle step's loop top (before its parameters) */ \
+      if (WAB_ROLL_THROTTLE && (wave == 0 || wave == 2)) __builtin_amdgcn_s_waitcnt(0x0F70);  \
       Params p = wave_params<G, FEAT>(p0);                                                   \
       step_slice(p, t);                                                                      \
       const SmallLayout L0 = small_layout(p);                                                \

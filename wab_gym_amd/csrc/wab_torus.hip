@@ -733,6 +733,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int nitems = (WAB2_ABLATE & 16) ? 0 : nvalid * nc;
           const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
           for (int rnd = wave; rnd * 64 < nitems; rnd += 4) {
+#if WAB2_STORE_THROTTLE >= 0
+            // (as at a mover round's start; the compiler's own wait tracking had put this one
+            // here already, from the action loads it carries as pending)
+            __builtin_amdgcn_s_waitcnt((WAB2_STORE_THROTTLE & 15) | ((WAB2_STORE_THROTTLE >> 4) << 14) | 0x0F70);
+#endif
             const int q = rnd * 64 + lane;
             const bool on = q < nitems;
             const int qc = on ? q : nitems - 1;
@@ -1088,6 +1093,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           const int nitems = (WAB2_ABLATE & 16) ? 0 : nvalid * nc;
           const int sh = bb & 3, d0 = bb >> 2, ndw = (sh + NB + 3) >> 2;
           for (int rnd = wave; rnd * 64 < nitems; rnd += 4) {
+#if WAB2_STORE_THROTTLE >= 0
+            // (as at a mover round's start; the compiler's own wait tracking had put this one
+            // here already, from the action loads it carries as pending)
+            __builtin_amdgcn_s_waitcnt((WAB2_STORE_THROTTLE & 15) | ((WAB2_STORE_THROTTLE >> 4) << 14) | 0x0F70);
+#endif
             const int q = rnd * 64 + lane;
             const bool on = q < nitems;
             const int qc = on ? q : nitems - 1;
